@@ -1,0 +1,472 @@
+// api.cpp -- the extern "C" boundary of libfpm_hip.so (include/fpm_hip.h).
+//
+// Mirrors runFPM(FPM_Dataset*) (fpmMain.cpp:274-498): fpm_init performs the
+// pupil/spectrum initialisation (fpmMain.cpp:302-343), fpm_run the
+// itrCount x ledUsedCount update loop and the per-iteration objCrop IDFT
+// (fpmMain.cpp:345-482), fpm_download hands back objF / objCrop / pupil /
+// pupilSupport in the reference's conventions.  Errors are negative codes plus
+// fpm_last_error(); nothing here ever falls back to a CPU path.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fpm_hip.h"
+#include "fft_lds.hpp"
+#include "fpm_state.hpp"
+
+namespace fpm {
+hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
+                               const float2 *tw, hipStream_t s);
+hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
+                            int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
+                            int out_es, int sroll, int iroll, float scale, hipStream_t s);
+hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const FftPlan &pl_np,
+                       const float2 *tw_np, hipStream_t s);
+hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
+                          hipStream_t s);
+// fused path (fpm_fused.hip)
+bool fused_supported(int np, int r, int L);
+hipError_t fused_prepare(const DevState &st, uint16_t *meas_perm, hipStream_t s);
+hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas_perm, const int *order_dev,
+                                  const int *x0_dev, const int *y0_dev, int n_order, hipStream_t s);
+size_t fused_meas_bytes(int np, int B, int n_stack);
+}  // namespace fpm
+
+using namespace fpm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return set_err(FPM_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                                \
+    } while (0)
+
+bool make_plan(int n, FftPlan *pl) {
+    std::memset(pl, 0, sizeof *pl);
+    pl->n = n;
+    int m = n, k = 0;
+    while (m % 4 == 0) { pl->radix[k++] = 4; m /= 4; }
+    while (m % 2 == 0) { pl->radix[k++] = 2; m /= 2; }
+    while (m % 3 == 0) { pl->radix[k++] = 3; m /= 3; }
+    while (m % 5 == 0) { pl->radix[k++] = 5; m /= 5; }
+    pl->nstages = k;
+    return m == 1 && k < 24;
+}
+
+std::vector<float2> twiddles(int n) {
+    std::vector<float2> t(n);
+    for (int k = 0; k < n; ++k) {
+        const double a = -2.0 * M_PI * (double)k / (double)n;
+        t[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    return t;
+}
+
+}  // namespace
+
+struct fpm_ctx {
+    fpm_problem prob{};
+    std::vector<int32_t> order, x0, y0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    DevState st{};
+    int path = FPM_PATH_GENERAL;
+    int support_px = 0;
+    FftPlan pl_np{}, pl_L{};
+    float2 *tw_np = nullptr, *tw_L = nullptr;
+    float2 *objcrop = nullptr;
+    uint16_t *meas = nullptr;
+    uint16_t *meas_perm = nullptr;  // fused-path layout
+    int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
+    uint8_t *disk_dev = nullptr;
+    std::vector<void *> allocs;
+    size_t bytes = 0;
+    bool uploaded = false, initialized = false, objcrop_valid = false;
+    std::vector<hipEvent_t> evpool;
+    fpm_timing timing{};
+};
+
+namespace {
+
+template <typename T>
+int dalloc(fpm_ctx *c, T **p, size_t count) {
+    void *q = nullptr;
+    const size_t nb = count * sizeof(T);
+    hipError_t e = hipMalloc(&q, nb > 0 ? nb : 16);
+    if (e != hipSuccess) return set_err(FPM_ERR_NOMEM, "hipMalloc(%zu) failed: %s", nb, hipGetErrorString(e));
+    c->allocs.push_back(q);
+    c->bytes += nb;
+    *p = (T *)q;
+    return FPM_OK;
+}
+
+void free_all(fpm_ctx *c) {
+    for (void *p : c->allocs) (void)hipFree(p);
+    c->allocs.clear();
+    for (auto e : c->evpool) (void)hipEventDestroy(e);
+    c->evpool.clear();
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+}
+
+int validate(const fpm_problem *p) {
+    if (!p) return set_err(FPM_ERR_INVAL, "null problem");
+    if (p->np < 4 || (p->np & 1)) return set_err(FPM_ERR_INVAL, "Np=%d must be even and >= 4", p->np);
+    if (p->nlarge < p->np || (p->nlarge & 1))
+        return set_err(FPM_ERR_INVAL, "Nlarge=%d must be even and >= Np", p->nlarge);
+    FftPlan t;
+    if (!make_plan(p->np, &t)) return set_err(FPM_ERR_INVAL, "Np=%d is not 2^a 3^b 5^c", p->np);
+    if (!make_plan(p->nlarge, &t)) return set_err(FPM_ERR_INVAL, "Nlarge=%d is not 2^a 3^b 5^c", p->nlarge);
+    if (p->na_radius < 0 || 2 * p->na_radius + 1 > p->np)
+        return set_err(FPM_ERR_INVAL, "naRadius=%d needs 2r+1 <= Np=%d", p->na_radius, p->np);
+    if (p->n_stack < 1 || p->n_order < 2)
+        return set_err(FPM_ERR_INVAL, "need n_stack>=1 and ledUsedCount>=2 (init uses sortedIndicies.at(1))");
+    if (!p->order || !p->crop_x0 || !p->crop_y0) return set_err(FPM_ERR_INVAL, "null order/crop arrays");
+    if (p->init_pos < 0 || p->init_pos >= p->n_order) return set_err(FPM_ERR_INVAL, "init_pos out of range");
+    if (!(p->delta2 > 0.0))
+        return set_err(FPM_ERR_INVAL, "delta2=%g: the reference divides 0/0 outside the support when delta2==0",
+                       p->delta2);
+    if (!(p->delta1 > 0.0)) return set_err(FPM_ERR_INVAL, "delta1=%g must be > 0", p->delta1);
+    if (p->n_patch < 1) return set_err(FPM_ERR_INVAL, "n_patch=%d", p->n_patch);
+    for (int i = 0; i < p->n_order; ++i)
+        if (p->order[i] < 0 || p->order[i] >= p->n_stack)
+            return set_err(FPM_ERR_INVAL, "order[%d]=%d outside the stack", i, p->order[i]);
+    for (int i = 0; i < p->n_stack; ++i) {
+        // cv::Rect(cropXStart, cropYStart, Np, Np) must lie inside objF (fpmMain.cpp:361)
+        if (p->crop_x0[i] < 0 || p->crop_x0[i] > p->nlarge - p->np || p->crop_y0[i] < 0 ||
+            p->crop_y0[i] > p->nlarge - p->np)
+            return set_err(FPM_ERR_INVAL, "LED %d crop (%d,%d) leaves the %dx%d spectrum", i, p->crop_x0[i],
+                           p->crop_y0[i], p->nlarge, p->nlarge);
+    }
+    return FPM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *fpm_last_error(void) { return g_err.c_str(); }
+
+const char *fpm_version(void) { return "libfpm_hip 0.1 (gfx950, fp32 complex state)"; }
+
+int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
+    if (!out) return set_err(FPM_ERR_INVAL, "null out");
+    *out = nullptr;
+    int rc = validate(prob);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(FPM_ERR_NODEV, "no HIP device visible");
+    if (device < 0 || device >= ndev) return set_err(FPM_ERR_NODEV, "device %d of %d", device, ndev);
+    hipDeviceProp_t pr;
+    HIP_TRY(hipGetDeviceProperties(&pr, device));
+    if (std::strncmp(pr.gcnArchName, "gfx950", 6) != 0)
+        return set_err(FPM_ERR_NODEV, "device %d is %s, this library is built for gfx950", device, pr.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+
+    fpm_ctx *c = new fpm_ctx();
+    c->prob = *prob;
+    c->device = device;
+    c->order.assign(prob->order, prob->order + prob->n_order);
+    c->x0.assign(prob->crop_x0, prob->crop_x0 + prob->n_stack);
+    c->y0.assign(prob->crop_y0, prob->crop_y0 + prob->n_stack);
+    c->prob.order = c->order.data();
+    c->prob.crop_x0 = c->x0.data();
+    c->prob.crop_y0 = c->y0.data();
+
+    auto fail = [&](int code) {
+        free_all(c);
+        delete c;
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(set_err(FPM_ERR_DEVICE, "hipStreamCreate failed"));
+    c->stream = c->own_stream;
+
+    const int np = prob->np, L = prob->nlarge, r = prob->na_radius, nb = 2 * r + 1, B = prob->n_patch;
+    DevState &st = c->st;
+    st.np = np;
+    st.L = L;
+    st.r = r;
+    st.nb = nb;
+    st.B = B;
+    st.ntx = (L + kTile - 1) / kTile;
+    st.nty = st.ntx;
+    st.delta1 = (float)prob->delta1;
+    st.delta2 = (float)prob->delta2;
+    st.eps = (float)prob->eps;
+    make_plan(np, &c->pl_np);
+    make_plan(L, &c->pl_L);
+
+    // support disk on the box: Euclidean disk == filled cv::circle (fpmMain.cpp:307)
+    std::vector<uint8_t> disk((size_t)nb * nb);
+    for (int i = 0; i < nb; ++i)
+        for (int j = 0; j < nb; ++j) {
+            const int ky = i - r, kx = j - r;
+            disk[(size_t)i * nb + j] = (ky * ky + kx * kx <= r * r) ? 1 : 0;
+            c->support_px += disk[(size_t)i * nb + j];
+        }
+
+    if (prob->path == FPM_PATH_FUSED && !fused_supported(np, r, L))
+        return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d", np, r, L));
+    c->path = (prob->path == FPM_PATH_GENERAL) ? FPM_PATH_GENERAL
+              : fused_supported(np, r, L)     ? FPM_PATH_FUSED
+                                              : FPM_PATH_GENERAL;
+
+    const size_t specn = (size_t)B * L * L;
+    if ((rc = dalloc(c, &st.spec, specn))) return fail(rc);
+    if ((rc = dalloc(c, &c->objcrop, specn))) return fail(rc);
+    if ((rc = dalloc(c, &st.pupil, (size_t)B * nb * nb))) return fail(rc);
+    if ((rc = dalloc(c, &st.tmax, (size_t)B * st.ntx * st.nty))) return fail(rc);
+    if ((rc = dalloc(c, &st.pmax, (size_t)B))) return fail(rc);
+    if ((rc = dalloc(c, &c->disk_dev, disk.size()))) return fail(rc);
+    if ((rc = dalloc(c, &c->meas, (size_t)prob->n_stack * B * np * np))) return fail(rc);
+    if ((rc = dalloc(c, &c->order_dev, (size_t)prob->n_order))) return fail(rc);
+    if ((rc = dalloc(c, &c->x0_dev, (size_t)prob->n_stack))) return fail(rc);
+    if ((rc = dalloc(c, &c->y0_dev, (size_t)prob->n_stack))) return fail(rc);
+    if (c->path == FPM_PATH_GENERAL) {
+        if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
+        if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
+    } else {
+        if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(uint16_t))))
+            return fail(rc);
+        if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
+    }
+    st.meas = c->meas;
+    st.disk = c->disk_dev;
+    auto twn = twiddles(np), twl = twiddles(L);
+    if ((rc = dalloc(c, &c->tw_np, twn.size()))) return fail(rc);
+    if ((rc = dalloc(c, &c->tw_L, twl.size()))) return fail(rc);
+    if (hipMemcpy(c->tw_np, twn.data(), twn.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->tw_L, twl.data(), twl.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->disk_dev, disk.data(), disk.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->order_dev, c->order.data(), c->order.size() * sizeof(int), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMemcpy(c->x0_dev, c->x0.data(), c->x0.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->y0_dev, c->y0.data(), c->y0.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(set_err(FPM_ERR_DEVICE, "table upload failed"));
+    *out = c;
+    return FPM_OK;
+}
+
+void fpm_destroy(fpm_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_all(c);
+    delete c;
+}
+
+int fpm_set_stream(fpm_ctx *c, void *s) {
+    if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return FPM_OK;
+}
+
+static int after_upload(fpm_ctx *c) {
+    if (c->path == FPM_PATH_FUSED) HIP_TRY(fused_prepare(c->st, c->meas_perm, c->stream));
+    c->uploaded = true;
+    c->initialized = false;
+    return FPM_OK;
+}
+
+int fpm_upload_stack(fpm_ctx *c, const uint16_t *meas) {
+    if (!c || !meas) return set_err(FPM_ERR_INVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = (size_t)c->prob.n_stack * c->st.B * c->st.np * c->st.np;
+    HIP_TRY(hipMemcpyAsync(c->meas, meas, n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return after_upload(c);
+}
+
+int fpm_upload_stack_device(fpm_ctx *c, const uint16_t *meas) {
+    if (!c || !meas) return set_err(FPM_ERR_INVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = (size_t)c->prob.n_stack * c->st.B * c->st.np * c->st.np;
+    HIP_TRY(hipMemcpyAsync(c->meas, meas, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, c->stream));
+    return after_upload(c);
+}
+
+int fpm_init(fpm_ctx *c) {
+    if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
+    if (!c->uploaded) return set_err(FPM_ERR_STATE, "fpm_init before fpm_upload_stack");
+    HIP_TRY(hipSetDevice(c->device));
+    const int init_led = c->order[c->prob.init_pos];
+    HIP_TRY(launch_init(c->st, init_led, c->objcrop, c->pl_np, c->tw_np, c->stream));
+    c->initialized = true;
+    c->objcrop_valid = false;
+    return FPM_OK;
+}
+
+int fpm_run(fpm_ctx *c, int iters) {
+    if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
+    if (!c->initialized) return set_err(FPM_ERR_STATE, "fpm_run before fpm_init");
+    if (iters < 0) return set_err(FPM_ERR_INVAL, "iters=%d", iters);
+    HIP_TRY(hipSetDevice(c->device));
+    const bool last_only = (c->prob.flags & FPM_FLAG_OBJCROP_LAST_ONLY) != 0;
+    // one event pair per iteration around the LED-update launches, one pair
+    // around the objCrop IDFT; read back once at the end (fpm_run is blocking)
+    const size_t need = 3 * (size_t)iters + 2;
+    while (c->evpool.size() < need) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->evpool.push_back(e);
+    }
+    hipEvent_t *ev = c->evpool.data();
+    HIP_TRY(hipEventRecord(ev[0], c->stream));
+    for (int it = 0; it < iters; ++it) {
+        HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
+        if (c->path == FPM_PATH_FUSED) {
+            HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
+                                           c->prob.n_order, c->stream));
+        } else {
+            for (int i = 0; i < c->prob.n_order; ++i) {
+                const int led = c->order[i];
+                HIP_TRY(launch_general_step(c->st, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, c->stream));
+            }
+        }
+        HIP_TRY(hipEventRecord(ev[2 + 3 * it], c->stream));
+        if (!last_only || it == iters - 1) {
+            HIP_TRY(launch_objcrop(c->st, c->objcrop, c->pl_L, c->tw_L, c->stream));
+            c->objcrop_valid = true;
+        }
+        HIP_TRY(hipEventRecord(ev[3 + 3 * it], c->stream));
+    }
+    HIP_TRY(hipEventRecord(ev[need - 1], c->stream));
+    HIP_TRY(hipEventSynchronize(ev[need - 1]));
+    double led_ms = 0, crop_ms = 0;
+    for (int it = 0; it < iters; ++it) {
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, ev[1 + 3 * it], ev[2 + 3 * it]));
+        HIP_TRY(hipEventElapsedTime(&b, ev[2 + 3 * it], ev[3 + 3 * it]));
+        led_ms += a;
+        crop_ms += b;
+    }
+    float tot = 0;
+    HIP_TRY(hipEventElapsedTime(&tot, ev[0], ev[need - 1]));
+    c->timing.run_ms = tot;
+    c->timing.led_ms = led_ms;
+    c->timing.objcrop_ms = crop_ms;
+    c->timing.led_launches = (c->path == FPM_PATH_FUSED) ? iters : iters * c->prob.n_order;
+    c->timing.led_launch_ms = c->timing.led_launches ? led_ms / c->timing.led_launches : 0.0;
+    return FPM_OK;
+}
+
+int fpm_synchronize(fpm_ctx *c) {
+    if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return FPM_OK;
+}
+
+int fpm_download(fpm_ctx *c, float *objF, float *objCrop, float *pupil, float *support) {
+    if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
+    if (!c->initialized) return set_err(FPM_ERR_STATE, "fpm_download before fpm_init");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const DevState &st = c->st;
+    const int L = st.L, np = st.np, r = st.r, nb = st.nb, B = st.B;
+    const size_t ll = (size_t)L * L;
+    if (objF) {
+        // spec is centred; objF = fftShift(spec) (fpmMain.cpp:447)
+        std::vector<float2> h(ll);
+        for (int b = 0; b < B; ++b) {
+            HIP_TRY(hipMemcpy(h.data(), st.spec + b * ll, ll * sizeof(float2), hipMemcpyDeviceToHost));
+            float2 *o = (float2 *)objF + b * ll;
+            for (int y = 0; y < L; ++y)
+                for (int x = 0; x < L; ++x) o[(size_t)y * L + x] = h[(size_t)((y + L / 2) % L) * L + (x + L / 2) % L];
+        }
+    }
+    if (objCrop) {
+        if (!c->objcrop_valid) HIP_TRY(launch_objcrop(c->st, c->objcrop, c->pl_L, c->tw_L, c->stream));
+        c->objcrop_valid = true;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(objCrop, c->objcrop, B * ll * sizeof(float2), hipMemcpyDeviceToHost));
+    }
+    if (pupil || support) {
+        std::vector<float2> h((size_t)B * nb * nb);
+        HIP_TRY(hipMemcpy(h.data(), st.pupil, h.size() * sizeof(float2), hipMemcpyDeviceToHost));
+        for (int b = 0; b < B; ++b) {
+            if (pupil) {
+                // centred pupil (fftShift at fpmMain.cpp:496): P[Np/2+ky][Np/2+kx]
+                float2 *o = (float2 *)pupil + (size_t)b * np * np;
+                std::memset(o, 0, sizeof(float2) * np * np);
+                for (int i = 0; i < nb; ++i)
+                    for (int j = 0; j < nb; ++j) o[(size_t)(np / 2 + i - r) * np + np / 2 + j - r] = h[((size_t)b * nb + i) * nb + j];
+            }
+            if (support) {
+                float *o = support + (size_t)b * np * np;
+                std::memset(o, 0, sizeof(float) * np * np);
+                for (int i = 0; i < nb; ++i)
+                    for (int j = 0; j < nb; ++j) {
+                        const int ky = i - r, kx = j - r;
+                        if (ky * ky + kx * kx <= r * r) o[(size_t)((ky + np) % np) * np + (kx + np) % np] = 1.f;
+                    }
+            }
+        }
+    }
+    return FPM_OK;
+}
+
+int fpm_download_objcrop_device(fpm_ctx *c, float *dst) {
+    if (!c || !dst) return set_err(FPM_ERR_INVAL, "null argument");
+    if (!c->initialized) return set_err(FPM_ERR_STATE, "download before fpm_init");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->objcrop_valid) HIP_TRY(launch_objcrop(c->st, c->objcrop, c->pl_L, c->tw_L, c->stream));
+    c->objcrop_valid = true;
+    const size_t n = (size_t)c->st.B * c->st.L * c->st.L * sizeof(float2);
+    HIP_TRY(hipMemcpyAsync(dst, c->objcrop, n, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return FPM_OK;
+}
+
+int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
+    if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
+    info->path = c->path;
+    info->box = c->st.nb;
+    info->support_px = c->support_px;
+    info->device = c->device;
+    info->device_bytes = c->bytes;
+    return FPM_OK;
+}
+
+int fpm_get_timing(const fpm_ctx *c, fpm_timing *t) {
+    if (!c || !t) return set_err(FPM_ERR_INVAL, "null argument");
+    *t = c->timing;
+    return FPM_OK;
+}
+
+int fpm_runFPM(const fpm_problem *prob, int device, const uint16_t *meas, int iters, float *objF, float *objCrop,
+               float *pupil, float *support) {
+    fpm_ctx *c = nullptr;
+    int rc = fpm_create(prob, device, &c);
+    if (rc) return rc;
+    if (!(rc = fpm_upload_stack(c, meas)) && !(rc = fpm_init(c)) && !(rc = fpm_run(c, iters)))
+        rc = fpm_download(c, objF, objCrop, pupil, support);
+    std::string keep = g_err;
+    fpm_destroy(c);
+    g_err = keep;
+    return rc;
+}
+
+}  // extern "C"

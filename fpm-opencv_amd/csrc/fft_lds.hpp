@@ -1,0 +1,168 @@
+// fft_lds.hpp -- mixed-radix (2/3/4/5) Stockham FFT over LDS-resident
+// sequences, plus the complex helpers shared by every FPM kernel.
+//
+// Replaces the reference's cvComplex fft2/ifft2 and cv::dft calls
+// (fpmMain.cpp:325,365,394,481) for arbitrary sizes N = 2^a 3^b 5^c: this is
+// the general path.  The metric-config hot loop uses the register-resident
+// 16x16 four-step transform in fpm_fused.hip instead.
+//
+// Stockham autosort (no bit reversal): pass p with radix R and current
+// sub-transform length Ns maps butterfly j to
+//     v[r] = src[j + r*N/R] * w^(r*(j mod Ns)),   w = exp(-+2 pi i/(Ns R))
+//     dst[(j/Ns)*Ns*R + (j mod Ns) + r*Ns] = DFT_R(v)[r]
+// Twiddles come from a host-computed (double precision) table
+// tw[k] = exp(-2 pi i k/N); the inverse uses the conjugate.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace fpm {
+
+struct FftPlan {
+    int n;
+    int nstages;
+    int radix[24];
+};
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// multiply by -i (forward) or +i (inverse)
+template <bool INV>
+__device__ __forceinline__ float2 mul_mi(float2 a) {
+    return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+}
+__device__ __forceinline__ float cabs2(float2 a) { return a.x * a.x + a.y * a.y; }
+
+template <bool INV>
+__device__ __forceinline__ void dft2(float2 *v) {
+    float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(float2 *v) {
+    float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+    float2 s13 = cadd(v[1], v[3]), d13 = mul_mi<INV>(csub(v[1], v[3]));
+    v[0] = cadd(s02, s13);
+    v[2] = csub(s02, s13);
+    v[1] = cadd(d02, d13);
+    v[3] = csub(d02, d13);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft3(float2 *v) {
+    const float h = 0.86602540378443864676f;  // sqrt(3)/2
+    float2 t = cadd(v[1], v[2]);
+    float2 d = csub(v[1], v[2]);
+    float2 m = make_float2(v[0].x - 0.5f * t.x, v[0].y - 0.5f * t.y);
+    // forward: y1 = m - i h d, y2 = m + i h d
+    float2 ihd = INV ? make_float2(-h * d.y, h * d.x) : make_float2(h * d.y, -h * d.x);  // (-+i) h d
+    v[0] = cadd(v[0], t);
+    v[1] = cadd(m, ihd);
+    v[2] = csub(m, ihd);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft5(float2 *v) {
+    const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+    const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+    float2 t1 = cadd(v[1], v[4]), d1 = csub(v[1], v[4]);
+    float2 t2 = cadd(v[2], v[3]), d2 = csub(v[2], v[3]);
+    float2 a0 = v[0];
+    float2 r1 = make_float2(a0.x + c1 * t1.x + c2 * t2.x, a0.y + c1 * t1.y + c2 * t2.y);
+    float2 r2 = make_float2(a0.x + c2 * t1.x + c1 * t2.x, a0.y + c2 * t1.y + c1 * t2.y);
+    float2 q1 = make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y);
+    float2 q2 = make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y);
+    float2 iq1 = mul_mi<INV>(q1), iq2 = mul_mi<INV>(q2);
+    v[0] = cadd(a0, cadd(t1, t2));
+    v[1] = cadd(r1, iq1);
+    v[4] = csub(r1, iq1);
+    v[2] = cadd(r2, iq2);
+    v[3] = csub(r2, iq2);
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void stockham_pass(const float2 *__restrict__ a, float2 *__restrict__ b,
+                                              int n, int C, int Ns, const float2 *__restrict__ tw,
+                                              int tid, int nthr) {
+    const int nR = n / R;
+    const int tmul = n / (Ns * R);
+    for (int jj = tid; jj < C * nR; jj += nthr) {
+        const int s = jj / nR;
+        const int j = jj - s * nR;
+        const float2 *src = a + s * n;
+        float2 *dst = b + s * n;
+        const int k = j % Ns;
+        float2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = src[j + r * nR];
+        if (Ns > 1) {
+            const int ts = tmul * k;
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                float2 w = tw[r * ts];
+                if (INV) w.y = -w.y;
+                v[r] = cmul(v[r], w);
+            }
+        }
+        if (R == 2) dft2<INV>(v);
+        if (R == 3) dft3<INV>(v);
+        if (R == 4) dft4<INV>(v);
+        if (R == 5) dft5<INV>(v);
+        const int base = (j / Ns) * Ns * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[base + r * Ns] = v[r];
+    }
+}
+
+// Transforms C sequences of length pl.n stored contiguously (sequence s at
+// a + s*n) in LDS; `b` is an equally sized ping-pong buffer.  Unscaled.
+// Returns the buffer that holds the result.  All threads of the block must
+// call it; it ends with a barrier.
+template <bool INV>
+__device__ float2 *stockham(float2 *a, float2 *b, int C, const FftPlan &pl,
+                            const float2 *__restrict__ tw, int tid, int nthr) {
+    int Ns = 1;
+    const int n = pl.n;
+    for (int st = 0; st < pl.nstages; ++st) {
+        const int R = pl.radix[st];
+        switch (R) {
+            case 4: stockham_pass<4, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
+            case 2: stockham_pass<2, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
+            case 3: stockham_pass<3, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
+            default: stockham_pass<5, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
+        }
+        __syncthreads();
+        float2 *t = a; a = b; b = t;
+        Ns *= R;
+    }
+    return a;
+}
+
+// ---- block reductions -------------------------------------------------------
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Max over the block; `red` is LDS scratch of >= nwaves floats. Result valid
+// in every thread. Contains two barriers.
+__device__ __forceinline__ float block_max(float v, float *red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nw = (blockDim.x + 63) >> 6;
+    v = wave_max(v);
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < nw; ++i) r = fmaxf(r, red[i]);
+    __syncthreads();
+    return r;
+}
+
+}  // namespace fpm

@@ -1,0 +1,41 @@
+// fpm_state.hpp -- device-resident solver state shared by the kernels.
+//
+// HBM layout (per context, n_patch = B patches):
+//   spec   float2 [B][L][L]     CENTRED high-resolution spectrum (objF after
+//                               fftShift).  Storing it centred removes the three
+//                               full-spectrum fftShift copies per LED the
+//                               reference makes (fpmMain.cpp:358,427,447): the
+//                               sub-aperture is a plain window at
+//                               (crop_y0 + Np/2 + ky, crop_x0 + Np/2 + kx).
+//   pupil  float2 [B][nb][nb]   pupil on its support box, ky,kx in [-r, r]
+//                               (un-centred frequencies, DC at [r][r]).  P is
+//                               zero outside the support forever
+//                               (fpmMain.cpp:312,472), so the Np x Np pupil is
+//                               never stored densely.
+//   meas   u16    [nS][B][Np][Np]  LED-major measurement stack.
+//   tmax   float  [B][nty][ntx] max |spec| per 16x16 tile: the exact global
+//                               max|objF| of fpmMain.cpp:460,467 without an
+//                               L x L pass per LED.
+//   pmax   float  [B]           max |P| (fpmMain.cpp:415) for the next LED.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fpm {
+
+constexpr int kTile = 16;
+
+struct DevState {
+    float2 *spec;
+    float2 *pupil;
+    const uint16_t *meas;
+    float2 *T;        // [B][nb][Np] row-transform scratch (general path)
+    float2 *dP;       // [B][nb][nb] pupil-update numerator (general path)
+    float *tmax;      // [B][nty][ntx]
+    float *pmax;      // [B]
+    const uint8_t *disk;  // [nb][nb] support mask
+    int np, L, r, nb, B, ntx, nty;
+    float delta1, delta2, eps;
+};
+
+}  // namespace fpm

@@ -1,0 +1,343 @@
+// general.hip -- the general (any Np = 2^a 3^b 5^c, any pupil radius) path of
+// the per-LED update, fpmMain.cpp:348-476, as four batched kernels per LED
+// step.  Every launch covers all B patches of the context.
+//
+//   K1 k_gather_rowifft   sub-aperture gather x pupil, row IDFTs over the
+//                         support box rows          (fpmMain.cpp:358-365)
+//   K2 k_colpass          column IDFT, amplitude replacement, column DFT,
+//                         only the box rows kept   (fpmMain.cpp:365-394)
+//   K3 k_rowfft_update    row DFT of the box rows, object update written to
+//                         the centred spectrum, pupil-update numerator
+//                                                   (fpmMain.cpp:394-447,457-464)
+//   K4 k_pupil_commit     tile maxima of |spec| under the ROI -> exact
+//                         max|objF|, P += num/max * S, max|P| for the next LED
+//                                                   (fpmMain.cpp:459-475,415)
+//
+// Pruning: P vanishes outside the support disk, so the inverse transform has
+// nonzero input only on the (2r+1)^2 box and only the box outputs of the
+// forward transform are ever used.  Row passes therefore run on nb = 2r+1 rows,
+// not Np.
+#include "fft_lds.hpp"
+#include "fpm_state.hpp"
+
+namespace fpm {
+
+struct StepArgs {
+    int xc, yc;      // centre of the sub-aperture in the centred spectrum
+    int led;         // stack index
+};
+
+// ---- K1 ---------------------------------------------------------------------
+// grid (nb, B), block 256, LDS 2*Np float2
+__global__ void __launch_bounds__(256) k_gather_rowifft(DevState st, StepArgs sa, FftPlan pl,
+                                                        const float2 *__restrict__ tw) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int np = st.np, r = st.r, nb = st.nb;
+    const int row = blockIdx.x, b = blockIdx.y;
+    const int ky = row - r;
+    float2 *bufa = smem, *bufb = smem + np;
+    const float2 *spec = st.spec + (size_t)b * st.L * st.L;
+    const float2 *pup = st.pupil + (size_t)b * nb * nb;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) bufa[i] = make_float2(0.f, 0.f);
+    __syncthreads();
+    const int yrow = sa.yc + ky;
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+        if (st.disk[row * nb + j]) {
+            const int kx = j - r;
+            float2 o = spec[(size_t)yrow * st.L + sa.xc + kx];
+            float2 p = pup[row * nb + j];
+            bufa[(kx + np) % np] = cmul(o, p);
+        }
+    }
+    __syncthreads();
+    float2 *res = stockham<true>(bufa, bufb, 1, pl, tw, threadIdx.x, blockDim.x);
+    float2 *T = st.T + ((size_t)b * nb + row) * np;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) T[i] = res[i];
+}
+
+// ---- K2 ---------------------------------------------------------------------
+// grid (Np, B), block 256, LDS 2*Np float2. One column per block.
+__global__ void __launch_bounds__(256) k_colpass(DevState st, StepArgs sa, FftPlan pl,
+                                                 const float2 *__restrict__ tw) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int np = st.np, r = st.r, nb = st.nb;
+    const int x = blockIdx.x, b = blockIdx.y;
+    float2 *bufa = smem, *bufb = smem + np;
+    float2 *T = st.T + (size_t)b * nb * np;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) bufa[i] = make_float2(0.f, 0.f);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) bufa[(j - r + np) % np] = T[(size_t)j * np + x];
+    __syncthreads();
+    float2 *res = stockham<true>(bufa, bufb, 1, pl, tw, threadIdx.x, blockDim.x);
+    float2 *oth = (res == bufa) ? bufb : bufa;
+    // amplitude replacement, fpmMain.cpp:378-393:
+    //   psi = ifft2(.) (1/Np^2 scale), psi' = sqrt(I) * psi / |psi + eps| (eps on Re)
+    const float inv_n2 = 1.0f / ((float)np * (float)np);
+    const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
+    for (int y = threadIdx.x; y < np; y += blockDim.x) {
+        float2 psi = cscale(res[y], inv_n2);
+        float a = sqrtf((float)I[(size_t)y * np + x]);
+        float tre = psi.x + st.eps;
+        float mag = sqrtf(tre * tre + psi.y * psi.y);
+        float s = a / mag;
+        res[y] = make_float2(psi.x * s, psi.y * s);
+    }
+    __syncthreads();
+    res = stockham<false>(res, oth, 1, pl, tw, threadIdx.x, blockDim.x);
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) T[(size_t)j * np + x] = res[(j - r + np) % np];
+}
+
+// ---- K3 ---------------------------------------------------------------------
+// grid (nb, B), block 256, LDS 2*Np float2
+__global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa, FftPlan pl,
+                                                       const float2 *__restrict__ tw) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int np = st.np, r = st.r, nb = st.nb;
+    const int row = blockIdx.x, b = blockIdx.y;
+    const int ky = row - r;
+    float2 *bufa = smem, *bufb = smem + np;
+    const float2 *T = st.T + ((size_t)b * nb + row) * np;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) bufa[i] = T[i];
+    __syncthreads();
+    float2 *res = stockham<false>(bufa, bufb, 1, pl, tw, threadIdx.x, blockDim.x);
+    float2 *spec = st.spec + (size_t)b * st.L * st.L;
+    float2 *pup = st.pupil + (size_t)b * nb * nb;
+    float2 *dP = st.dP + (size_t)b * nb * nb;
+    const float pm = st.pmax[b];
+    const int yrow = sa.yc + ky;
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+        if (!st.disk[row * nb + j]) continue;
+        const int kx = j - r;
+        const size_t si = (size_t)yrow * st.L + sa.xc + kx;
+        const float2 o = spec[si];               // pre-update Objfcrop (:361)
+        const float2 p = pup[row * nb + j];
+        const float2 F = res[(kx + np) % np];    // Objfup (:394)
+        const float2 D = csub(F, cmul(o, p));    // Objfup - ObjfcropP (:409,463)
+        // object update (:406-419,433): D |P| P* / ((|P|^2 + d2) max|P|)
+        const float pa = sqrtf(cabs2(p));
+        const float den_o = (pa * pa + st.delta2) * pm;
+        const float2 dpc = cmul(D, cscale(cconj(p), pa));
+        spec[si] = make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o);
+        // pupil numerator (:459-464,469): D |O| O* / (|O|^2 + d1); max|objF| in K4
+        const float oa = sqrtf(cabs2(o));
+        const float den_p = oa * oa + st.delta1;
+        const float2 n = cmul(D, cscale(cconj(o), oa));
+        dP[row * nb + j] = make_float2(n.x / den_p, n.y / den_p);
+    }
+}
+
+// ---- K4 ---------------------------------------------------------------------
+// grid (B), block 1024
+__global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa) {
+    __shared__ float red[32];
+    __shared__ float tred[4][4];
+    const int r = st.r, nb = st.nb, L = st.L;
+    const int b = blockIdx.x;
+    const float2 *spec = st.spec + (size_t)b * L * L;
+    float *tmax = st.tmax + (size_t)b * st.nty * st.ntx;
+    // 1. refresh the tile maxima under the ROI box (only those pixels changed)
+    const int ty0 = (sa.yc - r) / kTile, ty1 = (sa.yc + r) / kTile;
+    const int tx0 = (sa.xc - r) / kTile, tx1 = (sa.xc + r) / kTile;
+    const int ntw = tx1 - tx0 + 1, nt = (ty1 - ty0 + 1) * ntw;
+    const int q = threadIdx.x >> 8, qt = threadIdx.x & 255;
+    const int lane = threadIdx.x & 63, wq = (threadIdx.x >> 6) & 3;
+    for (int t0 = 0; t0 < nt; t0 += 4) {
+        const int t = t0 + q;
+        float m = 0.f;
+        int ty = 0, tx = 0;
+        if (t < nt) {
+            ty = ty0 + t / ntw;
+            tx = tx0 + t % ntw;
+            const int y = ty * kTile + (qt >> 4), x = tx * kTile + (qt & 15);
+            if (y < L && x < L) m = sqrtf(cabs2(spec[(size_t)y * L + x]));
+        }
+        m = wave_max(m);
+        if (lane == 0) tred[q][wq] = m;
+        __syncthreads();
+        if (t < nt && qt == 0)
+            tmax[ty * st.ntx + tx] = fmaxf(fmaxf(tred[q][0], tred[q][1]), fmaxf(tred[q][2], tred[q][3]));
+        __syncthreads();
+    }
+    // make this block's tile writes visible to its own later loads
+    __threadfence_block();
+    __syncthreads();
+    // 2. global max|objF| (fpmMain.cpp:467)
+    float m = 0.f;
+    for (int i = threadIdx.x; i < st.ntx * st.nty; i += blockDim.x) m = fmaxf(m, tmax[i]);
+    const float omax = block_max(m, red);
+    // 3. P += num / max * S (fpmMain.cpp:470-475); 4. max|P| for the next LED
+    float2 *pup = st.pupil + (size_t)b * nb * nb;
+    const float2 *dP = st.dP + (size_t)b * nb * nb;
+    float pm = 0.f;
+    for (int i = threadIdx.x; i < nb * nb; i += blockDim.x) {
+        if (!st.disk[i]) continue;
+        float2 p = pup[i];
+        const float2 d = dP[i];
+        p.x += d.x / omax;
+        p.y += d.y / omax;
+        pup[i] = p;
+        pm = fmaxf(pm, sqrtf(cabs2(p)));
+    }
+    pm = block_max(pm, red);
+    if (threadIdx.x == 0) st.pmax[b] = pm;
+}
+
+// ---- init / output kernels -------------------------------------------------
+
+// Batched 1-D transforms of `nseq` sequences of length pl.n per patch.
+// element i of sequence s of patch b:
+//   in [b*in_bs + ((s+sroll)%nseq)*in_ss + ((i+iroll)%n)*in_es]
+//   out[b*out_bs + s*out_ss + i*out_es] = scale * DFT(in)[i]
+// grid (ceil(nseq/C), B), block 256, LDS 2*C*n float2
+template <bool INV>
+__global__ void __launch_bounds__(256) k_fft_batch(const float2 *in, float2 *out,
+                                                   FftPlan pl, const float2 *__restrict__ tw, int C,
+                                                   int nseq, size_t in_bs, int in_ss, int in_es,
+                                                   size_t out_bs, int out_ss, int out_es, int sroll,
+                                                   int iroll, float scale) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int n = pl.n;
+    const int s0 = blockIdx.x * C, b = blockIdx.y;
+    const int cs = min(C, nseq - s0);
+    float2 *bufa = smem, *bufb = smem + (size_t)C * n;
+    in += (size_t)b * in_bs;
+    out += (size_t)b * out_bs;
+    // coalesce along whichever index is contiguous in memory
+    if (in_es == 1) {
+        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
+            const int s = idx / n, i = idx - s * n;
+            const int gs = (s0 + s + sroll) % nseq, gi = (i + iroll) % n;
+            bufa[s * n + i] = in[(size_t)gs * in_ss + gi];
+        }
+    } else {
+        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
+            const int i = idx / cs, s = idx - i * cs;
+            const int gs = (s0 + s + sroll) % nseq, gi = (i + iroll) % n;
+            bufa[s * n + i] = in[(size_t)gs * in_ss + (size_t)gi * in_es];
+        }
+    }
+    for (int idx = cs * n + threadIdx.x; idx < C * n; idx += blockDim.x) bufa[idx] = make_float2(0.f, 0.f);
+    __syncthreads();
+    float2 *res = stockham<INV>(bufa, bufb, C, pl, tw, threadIdx.x, blockDim.x);
+    if (out_es == 1) {
+        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
+            const int s = idx / n, i = idx - s * n;
+            out[(size_t)(s0 + s) * out_ss + i] = cscale(res[s * n + i], scale);
+        }
+    } else {
+        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
+            const int i = idx / cs, s = idx - i * cs;
+            out[(size_t)(s0 + s) * out_ss + (size_t)i * out_es] = cscale(res[s * n + i], scale);
+        }
+    }
+}
+
+// sqrt of the init image as complex, fpmMain.cpp:319-322. grid (Np, B)
+__global__ void k_init_amp(const uint16_t *__restrict__ meas, float2 *__restrict__ out, int np, int B,
+                           int led, size_t out_bs) {
+    const int y = blockIdx.x, b = blockIdx.y;
+    const uint16_t *I = meas + ((size_t)led * B + b) * np * np + (size_t)y * np;
+    float2 *o = out + (size_t)b * out_bs + (size_t)y * np;
+    for (int x = threadIdx.x; x < np; x += blockDim.x) o[x] = make_float2(sqrtf((float)I[x]), 0.f);
+}
+
+// zero the spectrum, place fftShift(fft2(A) * S) at the centre
+// (fpmMain.cpp:326-343), P = S, max|P| = 1.  grid (nb, B)
+__global__ void k_init_place(DevState st, const float2 *__restrict__ F, size_t f_bs) {
+    const int row = blockIdx.x, b = blockIdx.y;
+    const int np = st.np, r = st.r, nb = st.nb, L = st.L;
+    const int ky = row - r;
+    float2 *spec = st.spec + (size_t)b * L * L;
+    float2 *pup = st.pupil + (size_t)b * nb * nb;
+    const float2 *f = F + (size_t)b * f_bs;
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+        const int kx = j - r;
+        const bool in = st.disk[row * nb + j];
+        if (in) spec[(size_t)(L / 2 + ky) * L + L / 2 + kx] = f[(size_t)((ky + np) % np) * np + (kx + np) % np];
+        pup[row * nb + j] = make_float2(in ? 1.f : 0.f, 0.f);
+    }
+    if (row == 0 && threadIdx.x == 0) st.pmax[b] = (st.disk[r * nb + r] ? 1.f : 0.f);
+}
+
+// tile maxima of |spec| from scratch. grid (ntx*nty, B), block 256
+__global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
+    __shared__ float red[8];
+    const int t = blockIdx.x, b = blockIdx.y, L = st.L;
+    const int ty = t / st.ntx, tx = t % st.ntx;
+    const int y = ty * kTile + (threadIdx.x >> 4), x = tx * kTile + (threadIdx.x & 15);
+    float m = 0.f;
+    if (y < L && x < L) m = sqrtf(cabs2(st.spec[(size_t)b * L * L + (size_t)y * L + x]));
+    m = block_max(m, red);
+    if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = m;
+}
+
+// ---- host-side launchers ----------------------------------------------------
+hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
+                               const float2 *tw, hipStream_t s) {
+    StepArgs sa;
+    sa.led = led;
+    sa.xc = x0 + st.np / 2;
+    sa.yc = y0 + st.np / 2;
+    const size_t lds = 2 * (size_t)st.np * sizeof(float2);
+    hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    hipLaunchKernelGGL(k_pupil_commit, dim3(st.B), dim3(1024), 0, s, st, sa);
+    return hipGetLastError();
+}
+
+int fft_seq_per_block(int n) {
+    // keep 2*C*n*8 bytes <= 64 KiB so several blocks fit per CU
+    int c = (int)(65536 / (16 * (size_t)n));
+    if (c > 16) c = 16;
+    if (c < 1) c = 1;
+    return c;
+}
+
+hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
+                            int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
+                            int out_es, int sroll, int iroll, float scale, hipStream_t s) {
+    const int C = fft_seq_per_block(pl.n);
+    const size_t lds = 2 * (size_t)C * pl.n * sizeof(float2);
+    dim3 grid((nseq + C - 1) / C, B);
+    if (inverse)
+        hipLaunchKernelGGL(k_fft_batch<true>, grid, dim3(256), lds, s, in, out, pl, tw, C, nseq, in_bs, in_ss,
+                           in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
+    else
+        hipLaunchKernelGGL(k_fft_batch<false>, grid, dim3(256), lds, s, in, out, pl, tw, C, nseq, in_bs, in_ss,
+                           in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const FftPlan &pl_np,
+                       const float2 *tw_np, hipStream_t s) {
+    const int np = st.np;
+    const size_t bs = (size_t)np * np;
+    hipLaunchKernelGGL(k_init_amp, dim3(np, st.B), dim3(256), 0, s, st.meas, scratch, np, st.B, init_led, bs);
+    // fft2: rows then columns, in place (fpmMain.cpp:325)
+    hipError_t e = launch_fft_batch(false, scratch, scratch, pl_np, tw_np, np, st.B, bs, np, 1, bs, np, 1, 0, 0,
+                                    1.f, s);
+    if (e != hipSuccess) return e;
+    e = launch_fft_batch(false, scratch, scratch, pl_np, tw_np, np, st.B, bs, 1, np, bs, 1, np, 0, 0, 1.f, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(st.spec, 0, (size_t)st.B * st.L * st.L * sizeof(float2), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_init_place, dim3(st.nb, st.B), dim3(256), 0, s, st, (const float2 *)scratch, bs);
+    hipLaunchKernelGGL(k_tile_max_all, dim3(st.ntx * st.nty, st.B), dim3(256), 0, s, st);
+    return hipGetLastError();
+}
+
+// objCrop = IDFT(objF)/L^2 with objF = fftShift(spec) (fpmMain.cpp:481):
+// rows of the rolled spectrum, then columns, scaled by 1/L^2.
+hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
+                          hipStream_t s) {
+    const int L = st.L;
+    const size_t bs = (size_t)L * L;
+    hipError_t e = launch_fft_batch(true, st.spec, out, pl_L, tw_L, L, st.B, bs, L, 1, bs, L, 1, L / 2, L / 2, 1.f,
+                                    s);
+    if (e != hipSuccess) return e;
+    return launch_fft_batch(true, out, out, pl_L, tw_L, L, st.B, bs, 1, L, bs, 1, L, 0, 0,
+                            1.0f / ((float)L * (float)L), s);
+}
+
+}  // namespace fpm

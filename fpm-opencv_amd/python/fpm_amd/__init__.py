@@ -1,0 +1,245 @@
+"""ctypes mirror of the libfpm_hip.so C ABI (include/fpm_hip.h).
+
+This is the Python face of the reference's ``runFPM(FPM_Dataset*)``
+(fpmMain.cpp:274): ``Solver`` owns one ``fpm_ctx`` on one GPU and exposes
+create / upload / init / run / download with numpy arrays, and ``run_fpm`` is
+the one-shot call.  Errors raise ``FpmError`` carrying the library's negative
+code and ``fpm_last_error()`` text.  There is no CPU fallback: if the HIP
+library cannot be loaded, ``load_library`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))          # fpm-opencv_amd/
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libfpm_hip.so")
+HOST_LIB = os.path.join(LIB_DIR, "libfpm_host.so")
+
+FPM_OK = 0
+FPM_ERR_INVAL = -22
+FPM_ERR_NOMEM = -12
+FPM_ERR_DEVICE = -5
+FPM_ERR_STATE = -71
+FPM_ERR_NODEV = -19
+
+PATH_AUTO, PATH_GENERAL, PATH_FUSED = 0, 1, 2
+FLAG_OBJCROP_LAST_ONLY = 1
+
+# every symbol include/fpm_hip.h declares
+HIP_SYMBOLS = (
+    "fpm_create", "fpm_destroy", "fpm_upload_stack", "fpm_upload_stack_device",
+    "fpm_init", "fpm_run", "fpm_synchronize", "fpm_download",
+    "fpm_download_objcrop_device", "fpm_set_stream", "fpm_get_info",
+    "fpm_get_timing", "fpm_runFPM", "fpm_last_error", "fpm_version",
+)
+
+
+class FpmError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"fpm error {code}: {msg}")
+        self.code = code
+
+
+class fpm_problem(C.Structure):
+    _fields_ = [
+        ("np", C.c_int32), ("nlarge", C.c_int32), ("n_stack", C.c_int32),
+        ("n_order", C.c_int32), ("order", C.POINTER(C.c_int32)),
+        ("crop_x0", C.POINTER(C.c_int32)), ("crop_y0", C.POINTER(C.c_int32)),
+        ("na_radius", C.c_int32), ("init_pos", C.c_int32),
+        ("delta1", C.c_double), ("delta2", C.c_double), ("eps", C.c_double),
+        ("n_patch", C.c_int32), ("path", C.c_int32), ("flags", C.c_uint32),
+    ]
+
+
+class fpm_info(C.Structure):
+    _fields_ = [("path", C.c_int32), ("box", C.c_int32), ("support_px", C.c_int32),
+                ("device", C.c_int32), ("device_bytes", C.c_size_t)]
+
+
+class fpm_timing(C.Structure):
+    _fields_ = [("run_ms", C.c_double), ("led_ms", C.c_double),
+                ("led_launch_ms", C.c_double), ("led_launches", C.c_int32),
+                ("objcrop_ms", C.c_double)]
+
+
+_lib = None
+
+
+def load_library(path: str = HIP_LIB):
+    """Load libfpm_hip.so (raises OSError when it is missing -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not built: run `make -C fpm-opencv_amd` "
+                      "(or __graft_entry__.build())")
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    f32p = C.POINTER(C.c_float)
+    u16p = C.POINTER(C.c_uint16)
+    sig = {
+        "fpm_create": (C.c_int, [C.POINTER(fpm_problem), C.c_int, C.POINTER(vp)]),
+        "fpm_destroy": (None, [vp]),
+        "fpm_upload_stack": (C.c_int, [vp, u16p]),
+        "fpm_upload_stack_device": (C.c_int, [vp, vp]),
+        "fpm_init": (C.c_int, [vp]),
+        "fpm_run": (C.c_int, [vp, C.c_int]),
+        "fpm_synchronize": (C.c_int, [vp]),
+        "fpm_download": (C.c_int, [vp, f32p, f32p, f32p, f32p]),
+        "fpm_download_objcrop_device": (C.c_int, [vp, vp]),
+        "fpm_set_stream": (C.c_int, [vp, vp]),
+        "fpm_get_info": (C.c_int, [vp, C.POINTER(fpm_info)]),
+        "fpm_get_timing": (C.c_int, [vp, C.POINTER(fpm_timing)]),
+        "fpm_runFPM": (C.c_int, [C.POINTER(fpm_problem), C.c_int, u16p, C.c_int,
+                                 f32p, f32p, f32p, f32p]),
+        "fpm_last_error": (C.c_char_p, []),
+        "fpm_version": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != FPM_OK:
+        raise FpmError(rc, _lib.fpm_last_error().decode())
+
+
+def _i32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+
+def _f32p(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+@dataclass
+class Problem:
+    """Flattened ``FPM_Dataset`` fields runFPM reads."""
+    np_: int
+    L: int
+    order: np.ndarray
+    x0: np.ndarray
+    y0: np.ndarray
+    radius: int
+    delta1: float
+    delta2: float
+    n_patch: int = 1
+    init_pos: int = 1
+    eps: float = float(np.float32(1e-10))
+    path: int = PATH_AUTO
+    flags: int = 0
+    _keep: list = field(default_factory=list, repr=False)
+
+    def to_c(self) -> fpm_problem:
+        order, x0, y0 = _i32(self.order), _i32(self.x0), _i32(self.y0)
+        self._keep[:] = [order, x0, y0]
+        p = fpm_problem()
+        p.np = self.np_
+        p.nlarge = self.L
+        p.n_stack = len(x0)
+        p.n_order = len(order)
+        p.order = order.ctypes.data_as(C.POINTER(C.c_int32))
+        p.crop_x0 = x0.ctypes.data_as(C.POINTER(C.c_int32))
+        p.crop_y0 = y0.ctypes.data_as(C.POINTER(C.c_int32))
+        p.na_radius = self.radius
+        p.init_pos = self.init_pos
+        p.delta1 = float(self.delta1)
+        p.delta2 = float(self.delta2)
+        p.eps = float(self.eps)
+        p.n_patch = self.n_patch
+        p.path = self.path
+        p.flags = self.flags
+        return p
+
+
+class Solver:
+    """One fpm_ctx on one GPU."""
+
+    def __init__(self, prob: Problem, device: int = 0):
+        lib = load_library()
+        self.prob = prob
+        self._cprob = prob.to_c()
+        h = C.c_void_p()
+        _check(lib.fpm_create(C.byref(self._cprob), device, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.fpm_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def upload(self, stack: np.ndarray):
+        """stack: uint16 [n_stack][n_patch][Np][Np] (or [n_stack][Np][Np] if n_patch == 1)."""
+        p = self.prob
+        a = np.ascontiguousarray(stack, dtype=np.uint16)
+        want = (len(p.x0), p.n_patch, p.np_, p.np_)
+        if a.ndim == 3 and p.n_patch == 1:
+            a = a[:, None]
+        if a.shape != want:
+            raise ValueError(f"stack shape {a.shape} != {want}")
+        _check(_lib.fpm_upload_stack(self._h, a.ctypes.data_as(C.POINTER(C.c_uint16))))
+
+    def upload_device(self, ptr: int):
+        _check(_lib.fpm_upload_stack_device(self._h, C.c_void_p(ptr)))
+
+    def set_stream(self, stream_ptr: int | None):
+        _check(_lib.fpm_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    def init(self):
+        _check(_lib.fpm_init(self._h))
+
+    def run(self, iters: int):
+        _check(_lib.fpm_run(self._h, int(iters)))
+
+    def synchronize(self):
+        _check(_lib.fpm_synchronize(self._h))
+
+    def download(self, objF=True, objCrop=True, pupil=True, support=True):
+        p = self.prob
+        B, L, N = p.n_patch, p.L, p.np_
+        oF = np.empty((B, L, L), np.complex64) if objF else None
+        oC = np.empty((B, L, L), np.complex64) if objCrop else None
+        pu = np.empty((B, N, N), np.complex64) if pupil else None
+        su = np.empty((B, N, N), np.float32) if support else None
+        _check(_lib.fpm_download(self._h, _f32p(oF), _f32p(oC), _f32p(pu), _f32p(su)))
+        return dict(objF=oF, objCrop=oC, pupil=pu, support=su)
+
+    def download_objcrop_device(self, ptr: int):
+        _check(_lib.fpm_download_objcrop_device(self._h, C.c_void_p(ptr)))
+
+    def info(self) -> fpm_info:
+        i = fpm_info()
+        _check(_lib.fpm_get_info(self._h, C.byref(i)))
+        return i
+
+    def timing(self) -> fpm_timing:
+        t = fpm_timing()
+        _check(_lib.fpm_get_timing(self._h, C.byref(t)))
+        return t
+
+
+def run_fpm(prob: Problem, stack: np.ndarray, iters: int, device: int = 0):
+    """One-shot runFPM equivalent (create, upload, init, run, download)."""
+    with Solver(prob, device) as s:
+        s.upload(stack)
+        s.init()
+        s.run(iters)
+        return s.download()

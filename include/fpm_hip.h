@@ -1,0 +1,150 @@
+/*
+ * fpm_hip.h -- C ABI of the MI355X-native FPM solver (libfpm_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path
+ *     void runFPM(FPM_Dataset *dataset);      fpmMain.h:119, fpmMain.cpp:274-498
+ * which is called once from main after loadFPMDataset (fpmMain.cpp:590-591).
+ * FPM_Dataset is a C++ class full of cv::UMat, so the ABI flattens exactly the
+ * fields runFPM reads into plain integers, doubles and
+ * pointers; the outputs runFPM writes (objF, objCrop, pupil, pupilSupport) are
+ * copied out by fpm_download.  No torch or OpenCV types cross this boundary.
+ *
+ * Conventions
+ *   - complex arrays are interleaved float32 pairs (re, im), row-major;
+ *   - "stack index" = position of an LED image in the uploaded stack
+ *     (the reference indexes imageStack by LED number; the host front-end maps
+ *     LED numbers to stack indices, fpm_host.h);
+ *   - every call returns FPM_OK (0) or a negative errno-style code, and
+ *     fpm_last_error() describes the most recent failure on this thread;
+ *   - the caller owns host buffers, the library owns device buffers;
+ *   - one context per GPU; a context is not shared between threads.
+ */
+#ifndef FPM_HIP_H
+#define FPM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FPM_OK            0
+#define FPM_ERR_INVAL   (-22)   /* bad argument / unsupported geometry      */
+#define FPM_ERR_NOMEM   (-12)   /* device or host allocation failed          */
+#define FPM_ERR_DEVICE   (-5)   /* HIP runtime / kernel launch failure       */
+#define FPM_ERR_STATE   (-71)   /* call out of order (e.g. run before init)  */
+#define FPM_ERR_NODEV   (-19)   /* no usable gfx950 device                   */
+
+/* Solver path selection (fpm_problem.path). */
+#define FPM_PATH_AUTO     0     /* fused per-patch kernel when it applies    */
+#define FPM_PATH_GENERAL  1     /* 4 kernels per LED step, any Np / radius   */
+#define FPM_PATH_FUSED    2     /* one persistent launch per iteration       */
+
+/* fpm_problem.flags */
+#define FPM_FLAG_OBJCROP_LAST_ONLY 1u  /* compute objCrop only after the last
+                                          iteration of fpm_run (the reference
+                                          recomputes it every iteration,
+                                          fpmMain.cpp:481; default keeps that) */
+
+/*
+ * Problem description: the FPM_Dataset fields runFPM reads
+ * (fpmMain.h:43-101, read at fpmMain.cpp:290-481).
+ */
+typedef struct fpm_problem {
+    int32_t np;            /* Np: ROI size (cropSizeX, fpmMain.cpp:519); even    */
+    int32_t nlarge;        /* Nlarge == Mlarge == Np*resImprovementFactor (:564) */
+    int32_t n_stack;       /* images in the uploaded stack                       */
+    int32_t n_order;       /* ledUsedCount: LEDs processed per iteration (:348)  */
+    const int32_t *order;  /* [n_order] stack indices in processing order:
+                              sortedIndicies[0..ledUsedCount) (fpmMain.cpp:350)  */
+    const int32_t *crop_x0;/* [n_stack] cropXStart in the centred spectrum (:157) */
+    const int32_t *crop_y0;/* [n_stack] cropYStart (:163)                        */
+    int32_t na_radius;     /* naRadius = ceil(objNA*ps_eff*Np/lambda) (:305)     */
+    int32_t init_pos;      /* position in order[] of the init image; the
+                              reference uses sortedIndicies.at(1) (:319) -> 1    */
+    double  delta1;        /* pupil-update regulariser, JSON asInt (:567)         */
+    double  delta2;        /* object-update regulariser, JSON asInt (:568); > 0  */
+    double  eps;           /* amplitude-replacement eps, float 1e-10 (fpmMain.h:99) */
+    int32_t n_patch;       /* independent patches batched on this device (>= 1) */
+    int32_t path;          /* FPM_PATH_*                                          */
+    uint32_t flags;        /* FPM_FLAG_*                                          */
+} fpm_problem;
+
+typedef struct fpm_ctx fpm_ctx;
+
+/* Which path the context runs and its per-launch geometry. */
+typedef struct fpm_info {
+    int32_t path;          /* FPM_PATH_GENERAL or FPM_PATH_FUSED */
+    int32_t box;           /* 2*na_radius+1: side of the pupil box             */
+    int32_t support_px;    /* pixels in the pupil support disk                  */
+    int32_t device;
+    size_t  device_bytes;  /* device memory owned by the context               */
+} fpm_info;
+
+/* Per-kernel timing of the most recent fpm_run, from HIP events recorded on
+ * the stream the kernels were launched on. */
+typedef struct fpm_timing {
+    double run_ms;         /* whole fpm_run, event to event                    */
+    double led_ms;         /* LED-update kernels only (all iterations)         */
+    double led_launch_ms;  /* average duration of one LED-update launch        */
+    int32_t led_launches;  /* number of LED-update launches measured           */
+    double objcrop_ms;     /* per-iteration objCrop IDFT kernels               */
+} fpm_timing;
+
+/* Create a context on `device`; validates geometry, allocates device state. */
+int  fpm_create(const fpm_problem *prob, int device, fpm_ctx **out);
+void fpm_destroy(fpm_ctx *ctx);
+
+/* Upload the measurement stack, uint16 [n_stack][n_patch][Np][Np]
+ * (LED-major: every LED step reads one contiguous slab). Host pointer. */
+int  fpm_upload_stack(fpm_ctx *ctx, const uint16_t *meas);
+/* Same, from device memory on the context's device (no PCIe round trip). */
+int  fpm_upload_stack_device(fpm_ctx *ctx, const uint16_t *meas_dev);
+
+/* fpmMain.cpp:302-343: pupil = support disk, spectrum from order[init_pos]. */
+int  fpm_init(fpm_ctx *ctx);
+
+/* fpmMain.cpp:345-482: `iters` sequential passes over order[], each followed
+ * by the objCrop IDFT (fpmMain.cpp:481) unless FPM_FLAG_OBJCROP_LAST_ONLY.
+ * Enqueued on the context stream; returns when the work has completed
+ * (per-kernel HIP-event timings are then available from fpm_get_timing). */
+int  fpm_run(fpm_ctx *ctx, int iters);
+
+/* Wait for all work on the context stream. */
+int  fpm_synchronize(fpm_ctx *ctx);
+
+/* Copy results to host (any pointer may be NULL):
+ *   objF    [n_patch][L][L][2]   un-centred spectrum, like dataset->objF
+ *   objCrop [n_patch][L][L][2]   IDFT(objF)/L^2 (fpmMain.cpp:481)
+ *   pupil   [n_patch][Np][Np][2] centred pupil (fpmMain.cpp:496)
+ *   support [n_patch][Np][Np]    un-centred pupilSupport (real part, 0/1)  */
+int  fpm_download(fpm_ctx *ctx, float *objF, float *objCrop, float *pupil,
+                  float *support);
+
+/* Device-to-device copy of objCrop [n_patch][L][L][2] into caller memory on
+ * the context's device (for the multi-GPU gather). */
+int  fpm_download_objcrop_device(fpm_ctx *ctx, float *dst_dev);
+
+/* Use a caller-provided hipStream_t (NULL = the context's own stream). */
+int  fpm_set_stream(fpm_ctx *ctx, void *hip_stream);
+
+int  fpm_get_info(const fpm_ctx *ctx, fpm_info *info);
+int  fpm_get_timing(const fpm_ctx *ctx, fpm_timing *timing);
+
+/* One-shot equivalent of runFPM for n_patch patches: create, upload, init,
+ * run, download, destroy.  Blocking. */
+int  fpm_runFPM(const fpm_problem *prob, int device, const uint16_t *meas,
+                int iters, float *objF, float *objCrop, float *pupil,
+                float *support);
+
+/* Description of the most recent error on the calling thread. */
+const char *fpm_last_error(void);
+
+/* Library build identification (also proves the .so loaded). */
+const char *fpm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FPM_HIP_H */
