@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark: LED-updates/s of the MI355X FPM solver (BASELINE.json metric).
+
+Workload (SURVEY.md 8(d) metric config): dataset_dogStomach optics
+(6.5 um pixel, mag 8.1485, objNA 0.1, lambda 0.6292), all 293 LEDs of its
+holeCoordinates array (maxIlluminationNA raised to 0.6), cropSizeX Np = 256
+-> resImprovementFactor 3, L = 768, naRadius 33, delta1 = 10, delta2 = 3,
+256 independent patches per GPU (weak scaling: every rank owns its own 256
+patches), synthetic seeded forward-model stacks resident in HBM.
+
+One step = one runFPM iteration (fpmMain.cpp:345-482) over every patch:
+293 sequential LED updates per patch plus the per-iteration objCrop IDFT.
+value = patches x LEDs x steps x n_gpus / (max over ranks of the timed wall
+time).  Launch: `python bench.py` (1 GPU) or torch.distributed.run with
+--nproc-per-node N (one rank per GPU, RCCL).  After the timed region, ranks
+> 0 send their objCrop tiles to rank 0 with one RCCL gather (the stitched-field
+exchange of SURVEY.md 8(e)); its time is reported separately, not in value.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "fpm-opencv_amd", "python"), os.path.join(ROOT, "tests")]
+
+METRIC = "LED-updates/sec (patch·LED/s), 256² patch × 293 LEDs; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+F32_PEAK_TFLOPS = 157.3    # FP32 vector == FP32 MFMA dense peak (MI355X_MICROARCH.md)
+
+DOG_KEYS = {"cropSizeX": 256, "pixelSize": 6.5, "objectiveMag": 8.1485, "objectiveNA": 0.1,
+            "maxIlluminationNA": 0.6, "lambda": 0.6292, "delta1": 10, "delta2": 3,
+            "arrayRotation": 0, "flipDatasetX": False, "flipDatasetY": False}
+
+
+def metric_geometry(np_=256, max_na=0.6):
+    from fpm_amd import host
+    keys = dict(DOG_KEYS, cropSizeX=np_, maxIlluminationNA=max_na)
+    ds = host.Dataset(json_text=host.dataset_json(keys, host.dogstomach_led_table(), trailing_comma=True))
+    ds.set_present(range(1, 294))
+    n = ds.geometry()
+    cfg = ds.config()
+    x0, y0 = ds.crops()
+    return dict(np_=cfg.np, L=cfg.nlarge, r=cfg.na_radius, d1=cfg.delta1, d2=cfg.delta2, n_led=n,
+                order_leds=ds.order(), x0=x0, y0=y0)
+
+
+def algorithmic_flops_per_update(np_, nb, support_px):
+    """Flops of the support-pruned update per LED-update (DESIGN.md 'Roofline'):
+    5 N log2 N per executed 1-D DFT (nb row IDFTs, Np column IDFT+DFT pairs, nb
+    row DFTs), 12 flops/px amplitude replacement, 60 flops per support pixel for
+    the object + pupil updates."""
+    import math
+    lg = math.log2(np_)
+    return 5.0 * np_ * lg * (2 * nb + 2 * np_) + 12.0 * np_ * np_ + 60.0 * support_px
+
+
+def algorithmic_bytes_per_update(np_):
+    """read I (2) + read/write O ROI (8+8) + read/write P (8+8) per pixel."""
+    return 34.0 * np_ * np_
+
+
+def load_pmc(path, launch_kernel):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("per_launch_hbm_bytes", {}).get(launch_kernel)
+    except Exception:
+        return None
+
+
+def cpu_baseline(geo, stack_host, threads):
+    """C++ fp64 reference-faithful restatement (oracle/liboracle.so, 'port'),
+    one patch per thread, all 293 LEDs, one iteration; wall-clock."""
+    import numpy as np
+    import oracle_lib
+    order = np.arange(geo["n_led"], dtype=np.int32)
+    t0 = time.perf_counter()
+    oracle_lib.run_fpm_batch(stack_host, order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"],
+                             geo["d1"], geo["d2"], 1, threads, outputs=False)
+    dt = time.perf_counter() - t0
+    B = stack_host.shape[1]
+    return dict(value=B * geo["n_led"] / dt, unit="LED-updates/s", cores=threads, kind="port",
+                sample=f"{B} patches x {geo['n_led']} LEDs x 1 iteration, Np={geo['np_']} L={geo['L']}, "
+                       f"complex128, one patch per thread, {dt:.1f} s wall")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--patches", type=int, default=256, help="patches per GPU")
+    ap.add_argument("--np", type=int, default=256)
+    ap.add_argument("--path", default="auto", choices=["auto", "general", "fused"])
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import fpm_amd
+    from tools.synth_torch import make_stack
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    geo = metric_geometry(args.np)
+    B = args.patches
+    stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], B,
+                       seed=20261015 + 1000 * rank, device="cuda")
+    torch.cuda.synchronize()
+    path = {"auto": fpm_amd.PATH_AUTO, "general": fpm_amd.PATH_GENERAL, "fused": fpm_amd.PATH_FUSED}[args.path]
+    prob = fpm_amd.Problem(geo["np_"], geo["L"], np.arange(geo["n_led"]), geo["x0"], geo["y0"], geo["r"],
+                           geo["d1"], geo["d2"], n_patch=B, path=path)
+    solver = fpm_amd.Solver(prob, device=local)
+    solver.upload_device(stack.data_ptr())
+    solver.synchronize()
+    solver.init()
+    info = solver.info()
+
+    for _ in range(args.warmup):
+        solver.run(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    led_ms = 0.0
+    launches = 0
+    crop_ms = 0.0
+    for _ in range(args.steps):
+        solver.run(1)
+        t = solver.timing()
+        led_ms += t.led_ms
+        launches += t.led_launches
+        crop_ms += t.objcrop_ms
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    updates = B * geo["n_led"] * args.steps * world
+    value = updates / elapsed
+    per_launch_ms = led_ms / max(launches, 1)
+    per_launch_updates = B * geo["n_led"] if info.path == fpm_amd.PATH_FUSED else B
+    flops = algorithmic_flops_per_update(geo["np_"], info.box, info.support_px) * per_launch_updates
+    achieved_tf = flops / (per_launch_ms * 1e-3) / 1e12
+    kname = "k_fused_iteration" if info.path == fpm_amd.PATH_FUSED else "general_led_step(4 kernels)"
+    traffic = load_pmc(args.pmc, kname)
+    roofline = dict(bound="mfma", achieved=round(achieved_tf, 3), peak=F32_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(achieved_tf / F32_PEAK_TFLOPS, 4), traffic=traffic,
+                    kernel=kname, launch_ms=round(per_launch_ms, 4),
+                    flops_per_launch=flops,
+                    dense_equiv_hbm_GBs=round(algorithmic_bytes_per_update(geo["np_"]) * per_launch_updates
+                                              / (per_launch_ms * 1e-3) / 1e9, 1))
+
+    gather = None
+    if world > 1 and not args.no_gather:
+        L = geo["L"]
+        mine = torch.empty((B, L, L, 2), dtype=torch.float32, device="cuda")
+        solver.download_objcrop_device(mine.data_ptr())
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        glist = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+        dist.gather(mine, glist, dst=0)
+        torch.cuda.synchronize()
+        gms = (time.perf_counter() - g0) * 1e3
+        gather = dict(ms=round(gms, 2), GB_to_rank0=round(mine.numel() * 4 * (world - 1) / 1e9, 3))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        host_stack = stack[:, :threads].contiguous().cpu().numpy().view(np.uint16)
+        cpu = cpu_baseline(geo, host_stack, threads)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "LED-updates/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16",
+            "config": {"workload": "dataset_dogStomach optics, 293 LEDs (maxIlluminationNA 0.6), Np=256, "
+                                   "L=768, naRadius 33, one runFPM iteration per step",
+                       "patches_per_gpu": B, "leds": int(geo["n_led"]), "np": int(geo["np_"]),
+                       "nlarge": int(geo["L"]), "na_radius": int(geo["r"]),
+                       "path": "fused" if info.path == fpm_amd.PATH_FUSED else "general",
+                       "parallelism": f"patch-sharded x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "led_ms_per_step": round(led_ms / args.steps, 3),
+            "objcrop_ms_per_step": round(crop_ms / args.steps, 3),
+        }
+        if gather:
+            out["gather"] = gather
+        print(json.dumps(out), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
