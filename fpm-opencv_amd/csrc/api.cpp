@@ -31,10 +31,12 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
                           hipStream_t s);
 // fused path (fpm_fused.hip)
 bool fused_supported(int np, int r, int L);
-hipError_t fused_prepare(const DevState &st, uint16_t *meas_perm, hipStream_t s);
+hipError_t fused_permute(const uint16_t *meas, uint16_t *meas_perm, int n_stack, int B, hipStream_t s);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas_perm, const int *order_dev,
-                                  const int *x0_dev, const int *y0_dev, int n_order, hipStream_t s);
+                                  const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
+                                  hipStream_t s);
 size_t fused_meas_bytes(int np, int B, int n_stack);
+size_t fused_T_elems(int np, int r, int B);
 }  // namespace fpm
 
 using namespace fpm;
@@ -250,7 +252,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     } else {
         if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(uint16_t))))
             return fail(rc);
-        if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
+        if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
     }
     st.meas = c->meas;
     st.disk = c->disk_dev;
@@ -284,7 +286,8 @@ int fpm_set_stream(fpm_ctx *c, void *s) {
 }
 
 static int after_upload(fpm_ctx *c) {
-    if (c->path == FPM_PATH_FUSED) HIP_TRY(fused_prepare(c->st, c->meas_perm, c->stream));
+    if (c->path == FPM_PATH_FUSED)
+        HIP_TRY(fused_permute(c->meas, c->meas_perm, c->prob.n_stack, c->st.B, c->stream));
     c->uploaded = true;
     c->initialized = false;
     return FPM_OK;
@@ -338,7 +341,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
         if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
-                                           c->prob.n_order, c->stream));
+                                           c->prob.n_order, c->tw_np, c->stream));
         } else {
             for (int i = 0; i < c->prob.n_order; ++i) {
                 const int led = c->order[i];

@@ -88,3 +88,57 @@ def test_golden_fixtures_on_gpu():
         out = fpm_amd.run_fpm(prob, g["stack"], iters)
         for k in ("objF", "objCrop", "pupil"):
             assert rel_l2(out[k][0], g[k]) < _tol(iters), (path, k)
+
+
+FUSED_CASES = [
+    # r, n_side, step, iters: NB = 2r+1 rows; > 64 rows exercises the tail-row direct DFTs
+    (10, 5, 24, 2),
+    (31, 3, 40, 2),     # NB 63: every row on the FFT groups
+    (32, 3, 40, 2),     # NB 65: one tail row
+    (33, 5, 20, 2),     # NB 67: the metric radius, three tail rows
+    (34, 3, 30, 3),     # NB 69: five tail rows, 59 tail pixels
+]
+
+
+@pytest.mark.parametrize("case", FUSED_CASES, ids=lambda c: f"r{c[0]}_leds{c[1]**2}_it{c[3]}")
+def test_fused_path_matches_oracle(case):
+    r, nside, step, iters = case
+    Np, L = 256, 512
+    x0, y0, order = grid_geometry(Np, L, nside, step)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=21)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=2, path=fpm_amd.PATH_FUSED)
+    with fpm_amd.Solver(prob) as s:
+        assert s.info().path == fpm_amd.PATH_FUSED
+        s.upload(stack)
+        s.init()
+        s.run(iters)
+        out = s.download()
+    import oracle_lib
+    for b in range(2):
+        ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, 10, 3, iters)
+        assert rel_l2(out["objF"][b], ref["objF"]) < _tol(iters)
+        assert rel_l2(out["objCrop"][b], ref["objCrop"]) < _tol(iters)
+        assert rel_l2(out["pupil"][b], ref["pupil"]) < _tol(iters)
+
+
+def test_fused_equals_general_path():
+    """Both device paths on the same inputs agree to fp32 rounding."""
+    Np, L, r, iters = 256, 512, 33, 2
+    x0, y0, order = grid_geometry(Np, L, 5, 20)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=22)
+    outs = {}
+    for path in (fpm_amd.PATH_GENERAL, fpm_amd.PATH_FUSED):
+        prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, path=path)
+        outs[path] = fpm_amd.run_fpm(prob, stack, iters)
+    for k in ("objF", "objCrop", "pupil"):
+        assert rel_l2(outs[fpm_amd.PATH_FUSED][k], outs[fpm_amd.PATH_GENERAL][k]) < 2e-6
+
+
+def test_unsupported_fused_radius_falls_back_to_general():
+    Np, L, r = 256, 512, 40
+    x0, y0, order = grid_geometry(Np, L, 3, 30)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, path=fpm_amd.PATH_AUTO)
+    with fpm_amd.Solver(prob) as s:
+        assert s.info().path == fpm_amd.PATH_GENERAL
+    with pytest.raises(fpm_amd.FpmError):
+        fpm_amd.Solver(fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, path=fpm_amd.PATH_FUSED))
