@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--data", default="model", choices=["model", "random"],
+                    help="random: uniform uint16 stack (profiling runs only; not a bench number)")
     args = ap.parse_args()
 
     import numpy as np
@@ -117,8 +119,14 @@ def main():
 
     geo = metric_geometry(args.np)
     B = args.patches
-    stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], B,
-                       seed=20261015 + 1000 * rank, device="cuda")
+    if args.data == "random":
+        g = torch.Generator(device="cuda")
+        g.manual_seed(rank)
+        stack = torch.randint(0, 40000, (geo["n_led"], B, geo["np_"], geo["np_"]), generator=g, device="cuda",
+                              dtype=torch.int32).to(torch.int16)
+    else:
+        stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], B,
+                           seed=20261015 + 1000 * rank, device="cuda")
     torch.cuda.synchronize()
     path = {"auto": fpm_amd.PATH_AUTO, "general": fpm_amd.PATH_GENERAL, "fused": fpm_amd.PATH_FUSED}[args.path]
     prob = fpm_amd.Problem(geo["np_"], geo["L"], np.arange(geo["n_led"]), geo["x0"], geo["y0"], geo["r"],
@@ -193,7 +201,8 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "LED-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16",
+            "data": ("synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16"
+                     if args.data == "model" else "random uint16 (profiling only)"),
             "config": {"workload": "dataset_dogStomach optics, 293 LEDs (maxIlluminationNA 0.6), Np=256, "
                                    "L=768, naRadius 33, one runFPM iteration per step",
                        "patches_per_gpu": B, "leds": int(geo["n_led"]), "np": int(geo["np_"]),

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -34,7 +35,7 @@ bool fused_supported(int np, int r, int L);
 hipError_t fused_permute(const uint16_t *meas, uint16_t *meas_perm, int n_stack, int B, hipStream_t s);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas_perm, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  hipStream_t s);
+                                  unsigned long long *dbg, hipStream_t s);
 size_t fused_meas_bytes(int np, int B, int n_stack);
 size_t fused_T_elems(int np, int r, int B);
 }  // namespace fpm
@@ -106,6 +107,7 @@ struct fpm_ctx {
     size_t bytes = 0;
     bool uploaded = false, initialized = false, objcrop_valid = false;
     std::vector<hipEvent_t> evpool;
+    unsigned long long *dbg = nullptr;  // FPM_STAMPS=1: fused-kernel phase cycles
     fpm_timing timing{};
 };
 
@@ -240,6 +242,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &c->objcrop, specn))) return fail(rc);
     if ((rc = dalloc(c, &st.pupil, (size_t)B * nb * nb))) return fail(rc);
     if ((rc = dalloc(c, &st.tmax, (size_t)B * st.ntx * st.nty))) return fail(rc);
+    if ((rc = dalloc(c, &st.tdirty, (size_t)B * ((st.ntx * st.nty + 31) / 32)))) return fail(rc);
     if ((rc = dalloc(c, &st.pmax, (size_t)B))) return fail(rc);
     if ((rc = dalloc(c, &c->disk_dev, disk.size()))) return fail(rc);
     if ((rc = dalloc(c, &c->meas, (size_t)prob->n_stack * B * np * np))) return fail(rc);
@@ -256,6 +259,11 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     }
     st.meas = c->meas;
     st.disk = c->disk_dev;
+    if (getenv("FPM_STAMPS") && c->path == FPM_PATH_FUSED) {
+        if ((rc = dalloc(c, &c->dbg, 8))) return fail(rc);
+        if (hipMemset(c->dbg, 0, 8 * sizeof(unsigned long long)) != hipSuccess)
+            return fail(set_err(FPM_ERR_DEVICE, "memset failed"));
+    }
     auto twn = twiddles(np), twl = twiddles(L);
     if ((rc = dalloc(c, &c->tw_np, twn.size()))) return fail(rc);
     if ((rc = dalloc(c, &c->tw_L, twl.size()))) return fail(rc);
@@ -341,7 +349,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
         if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
-                                           c->prob.n_order, c->tw_np, c->stream));
+                                           c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else {
             for (int i = 0; i < c->prob.n_order; ++i) {
                 const int led = c->order[i];
@@ -371,6 +379,16 @@ int fpm_run(fpm_ctx *c, int iters) {
     c->timing.led_ms = led_ms;
     c->timing.objcrop_ms = crop_ms;
     c->timing.led_launches = (c->path == FPM_PATH_FUSED) ? iters : iters * c->prob.n_order;
+    if (c->dbg) {
+        unsigned long long h[8];
+        HIP_TRY(hipMemcpy(h, c->dbg, sizeof h, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(c->dbg, 0, sizeof h));
+        const double steps = (double)iters * c->prob.n_order * c->st.B;
+        fprintf(stderr, "[fpm stamps] cycles per LED step (wave 0 view, mean over blocks):");
+        const char *names[7] = {"A:rowIDFT", "A:tail", "B:columns", "C:rowDFT+upd", "C:tail", "D:tiles", "D:max+P"};
+        for (int i = 0; i < 7; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / steps);
+        fprintf(stderr, "\n");
+    }
     c->timing.led_launch_ms = c->timing.led_launches ? led_ms / c->timing.led_launches : 0.0;
     return FPM_OK;
 }

@@ -35,7 +35,9 @@ template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
     return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
 }
-__device__ __forceinline__ float cabs2(float2 a) { return a.x * a.x + a.y * a.y; }
+// |a|^2 with an explicit fma so every kernel rounds it identically (the fused
+// path compares tile maxima bit for bit with freshly computed magnitudes)
+__device__ __forceinline__ float cabs2(float2 a) { return __builtin_fmaf(a.x, a.x, a.y * a.y); }
 
 template <bool INV>
 __device__ __forceinline__ void dft2(float2 *v) {

@@ -32,6 +32,7 @@ struct DevState {
     float2 *T;        // [B][nb][Np] row-transform scratch (general path)
     float2 *dP;       // [B][nb][nb] pupil-update numerator (general path)
     float *tmax;      // [B][nty][ntx]
+    unsigned *tdirty; // [B][ceil(ntx*nty/32)] fused path: tiles whose max is an upper bound
     float *pmax;      // [B]
     const uint8_t *disk;  // [nb][nb] support mask
     int np, L, r, nb, B, ntx, nty;

@@ -324,6 +324,8 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_init_place, dim3(st.nb, st.B), dim3(256), 0, s, st, (const float2 *)scratch, bs);
     hipLaunchKernelGGL(k_tile_max_all, dim3(st.ntx * st.nty, st.B), dim3(256), 0, s, st);
+    e = hipMemsetAsync(st.tdirty, 0, (size_t)st.B * ((st.ntx * st.nty + 31) / 32) * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
