@@ -23,6 +23,7 @@
 namespace fpm {
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
                                const float2 *tw, hipStream_t s);
+int fft_max_len();
 hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
                             int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
                             int out_es, int sroll, int iroll, float scale, hipStream_t s);
@@ -141,6 +142,8 @@ int validate(const fpm_problem *p) {
     FftPlan t;
     if (!make_plan(p->np, &t)) return set_err(FPM_ERR_INVAL, "Np=%d is not 2^a 3^b 5^c", p->np);
     if (!make_plan(p->nlarge, &t)) return set_err(FPM_ERR_INVAL, "Nlarge=%d is not 2^a 3^b 5^c", p->nlarge);
+    if (p->nlarge > fft_max_len())
+        return set_err(FPM_ERR_INVAL, "Nlarge=%d exceeds the batched transform limit %d", p->nlarge, fft_max_len());
     if (p->na_radius < 0 || 2 * p->na_radius + 1 > p->np)
         return set_err(FPM_ERR_INVAL, "naRadius=%d needs 2r+1 <= Np=%d", p->na_radius, p->np);
     if (p->n_stack < 1 || p->n_order < 2)

@@ -88,18 +88,32 @@ __device__ __forceinline__ void dft5(float2 *v) {
     v[3] = csub(r2, iq2);
 }
 
+// a / d for 0 <= a < 2^22 via the float reciprocal rd = 1/d and one
+// correction step (an integer division by a runtime value costs ~40 VALU
+// instructions on CDNA; this is 6)
+__device__ __forceinline__ int udiv(int a, int d, float rd) {
+    int q = (int)((float)a * rd);
+    const int r = a - q * d;
+    q += (r >= d) - (r < 0);
+    return q;
+}
+
 template <int R, bool INV>
 __device__ __forceinline__ void stockham_pass(const float2 *__restrict__ a, float2 *__restrict__ b,
                                               int n, int C, int Ns, const float2 *__restrict__ tw,
                                               int tid, int nthr) {
     const int nR = n / R;
     const int tmul = n / (Ns * R);
+    const float rNs = 1.0f / (float)Ns, rnR = 1.0f / (float)nR;
+    const bool pow2 = (Ns & (Ns - 1)) == 0;
+    const int lNs = 31 - __builtin_clz(Ns);
     for (int jj = tid; jj < C * nR; jj += nthr) {
-        const int s = jj / nR;
+        const int s = (C == 1) ? 0 : udiv(jj, nR, rnR);
         const int j = jj - s * nR;
         const float2 *src = a + s * n;
         float2 *dst = b + s * n;
-        const int k = j % Ns;
+        const int jq = pow2 ? (j >> lNs) : udiv(j, Ns, rNs);
+        const int k = j - jq * Ns;
         float2 v[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) v[r] = src[j + r * nR];
@@ -116,7 +130,7 @@ __device__ __forceinline__ void stockham_pass(const float2 *__restrict__ a, floa
         if (R == 3) dft3<INV>(v);
         if (R == 4) dft4<INV>(v);
         if (R == 5) dft5<INV>(v);
-        const int base = (j / Ns) * Ns * R + k;
+        const int base = jq * Ns * R + k;
 #pragma unroll
         for (int r = 0; r < R; ++r) dst[base + r * Ns] = v[r];
     }

@@ -636,15 +636,26 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 
 // measurement permutation for coalesced column reads:
 // out[s][b][x][t][m2] = in[s][b][t + 16 m2][x]
-__global__ void k_permute_meas(const uint16_t *__restrict__ in, uint16_t *__restrict__ out, size_t nimg) {
+// One block transposes a 256(y) x 64(x) slab through LDS: coalesced 128-byte
+// row reads, then each output row x (256 contiguous values) is written by
+// consecutive threads.  grid (NP/64, nimg), block 256.
+__global__ void __launch_bounds__(256) k_permute_meas(const uint16_t *__restrict__ in, uint16_t *__restrict__ out,
+                                                      size_t nimg) {
+    __shared__ uint16_t tile[fz::NP][64 + 2];
     const size_t img = blockIdx.y;
     if (img >= nimg) return;
+    const int xs = blockIdx.x * 64;
     const uint16_t *src = in + img * fz::NP * fz::NP;
     uint16_t *dst = out + img * fz::NP * fz::NP;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < fz::NP * fz::NP; i += gridDim.x * blockDim.x) {
-        const int y = i / fz::NP, x = i % fz::NP;  // coalesced read
-        const int t = y & 15, m2 = y >> 4;
-        dst[((size_t)x * 16 + t) * 16 + m2] = src[i];
+    for (int i = threadIdx.x; i < fz::NP * 64; i += 256) {
+        const int y = i >> 6, x = i & 63;
+        tile[y][x] = src[(size_t)y * fz::NP + xs + x];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * fz::NP; i += 256) {
+        const int x = i >> 8, j = i & 255;
+        const int y = (j >> 4) + 16 * (j & 15);
+        dst[(size_t)(xs + x) * fz::NP + j] = tile[y][x];
     }
 }
 
@@ -703,7 +714,7 @@ hipError_t fused_permute(const uint16_t *meas, uint16_t *meas_perm, int n_stack,
     const size_t nimg = (size_t)n_stack * B;
     for (size_t i0 = 0; i0 < nimg; i0 += 65535) {
         const size_t n = (nimg - i0 < 65535) ? nimg - i0 : 65535;
-        hipLaunchKernelGGL(k_permute_meas, dim3(64, (unsigned)n), dim3(256), 0, s,
+        hipLaunchKernelGGL(k_permute_meas, dim3(fz::NP / 64, (unsigned)n), dim3(256), 0, s,
                            meas + i0 * fz::NP * fz::NP, meas_perm + i0 * fz::NP * fz::NP, n);
     }
     return hipGetLastError();

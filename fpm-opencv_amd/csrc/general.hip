@@ -188,47 +188,125 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
 // element i of sequence s of patch b:
 //   in [b*in_bs + ((s+sroll)%nseq)*in_ss + ((i+iroll)%n)*in_es]
 //   out[b*out_bs + s*out_ss + i*out_es] = scale * DFT(in)[i]
-// grid (ceil(nseq/C), B), block 256, LDS 2*C*n float2
-template <bool INV>
-__global__ void __launch_bounds__(256) k_fft_batch(const float2 *in, float2 *out,
-                                                   FftPlan pl, const float2 *__restrict__ tw, int C,
-                                                   int nseq, size_t in_bs, int in_ss, int in_es,
-                                                   size_t out_bs, int out_ss, int out_es, int sroll,
-                                                   int iroll, float scale) {
-    extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    const int n = pl.n;
-    const int s0 = blockIdx.x * C, b = blockIdx.y;
-    const int cs = min(C, nseq - s0);
-    float2 *bufa = smem, *bufb = smem + (size_t)C * n;
-    in += (size_t)b * in_bs;
-    out += (size_t)b * out_bs;
-    // coalesce along whichever index is contiguous in memory
-    if (in_es == 1) {
-        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
-            const int s = idx / n, i = idx - s * n;
-            const int gs = (s0 + s + sroll) % nseq, gi = (i + iroll) % n;
-            bufa[s * n + i] = in[(size_t)gs * in_ss + gi];
-        }
-    } else {
-        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
-            const int i = idx / cs, s = idx - i * cs;
-            const int gs = (s0 + s + sroll) % nseq, gi = (i + iroll) % n;
-            bufa[s * n + i] = in[(size_t)gs * in_ss + (size_t)gi * in_es];
+// A block owns C = 2^lc consecutive sequences.  When the sequences are
+// columns (in_es != 1) consecutive threads read consecutive sequences, so a
+// wave touches 16 rows x C*8 contiguous bytes; the LDS tile is then
+// sequence-interleaved (lss 1, les C).  For rows it is row-major with one pad
+// element per row (lss n+1, les 1) so the butterflies of C sequences hit
+// distinct banks.  The transform runs IN PLACE over one LDS buffer: every pass
+// lifts all of a thread's butterflies into registers, barriers, and stores
+// (<= kFftRegElems complex values per thread), so C*n can reach
+// kFftRegElems*blockDim without a ping-pong buffer.
+constexpr int kFftThreads = 512;
+constexpr int kFftRegElems = 24;
+
+template <int R, bool INV>
+__device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int lss, int les, int Ns,
+                                                 const float2 *__restrict__ tw) {
+    constexpr int Q = kFftRegElems / R;
+    const int nR = n / R, total = nR << lc, tmul = n / (Ns * R);
+    const bool pow2 = (Ns & (Ns - 1)) == 0;
+    const int lNs = 31 - __builtin_clz(Ns);
+    const float rNs = 1.0f / (float)Ns;
+    float2 v[Q][R];
+    int dst[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int jj = threadIdx.x + q * kFftThreads;
+        if (jj < total) {
+            const int sq = jj & ((1 << lc) - 1), j = jj >> lc;
+            const float2 *src = buf + sq * lss;
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[q][r] = src[(j + r * nR) * les];
+            const int jq = pow2 ? (j >> lNs) : udiv(j, Ns, rNs);
+            const int k = j - jq * Ns;
+            if (Ns > 1) {
+                const int ts = tmul * k;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    float2 w = tw[r * ts];
+                    if (INV) w.y = -w.y;
+                    v[q][r] = cmul(v[q][r], w);
+                }
+            }
+            if (R == 2) dft2<INV>(v[q]);
+            if (R == 3) dft3<INV>(v[q]);
+            if (R == 4) dft4<INV>(v[q]);
+            if (R == 5) dft5<INV>(v[q]);
+            dst[q] = sq * lss + (jq * Ns * R + k) * les;
         }
     }
-    for (int idx = cs * n + threadIdx.x; idx < C * n; idx += blockDim.x) bufa[idx] = make_float2(0.f, 0.f);
     __syncthreads();
-    float2 *res = stockham<INV>(bufa, bufb, C, pl, tw, threadIdx.x, blockDim.x);
-    if (out_es == 1) {
-        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
-            const int s = idx / n, i = idx - s * n;
-            out[(size_t)(s0 + s) * out_ss + i] = cscale(res[s * n + i], scale);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int jj = threadIdx.x + q * kFftThreads;
+        if (jj < total) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[dst[q] + r * Ns * les] = v[q][r];
         }
-    } else {
-        for (int idx = threadIdx.x; idx < cs * n; idx += blockDim.x) {
-            const int i = idx / cs, s = idx - i * cs;
-            out[(size_t)(s0 + s) * out_ss + (size_t)i * out_es] = cscale(res[s * n + i], scale);
+    }
+    __syncthreads();
+}
+
+template <bool INV>
+__global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, float2 *out, FftPlan pl,
+                                                           const float2 *__restrict__ tw, int lc, int nseq,
+                                                           size_t in_bs, int in_ss, int in_es, size_t out_bs,
+                                                           int out_ss, int out_es, int sroll, int iroll,
+                                                           float scale) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int n = pl.n, C = 1 << lc, cm = C - 1;
+    const int s0 = blockIdx.x << lc, b = blockIdx.y;
+    const int cs = min(C, nseq - s0);
+    const bool colmajor = in_es != 1;
+    const int lss = colmajor ? 1 : n + 1, les = colmajor ? C : 1;
+    const float rn = 1.0f / (float)n;
+    in += (size_t)b * in_bs;
+    out += (size_t)b * out_bs;
+    const int tot = n << lc;
+    // all of a thread's loads are issued before any LDS store so their
+    // latencies overlap (a rolled loop waits for each one in turn)
+    float2 v[kFftRegElems];
+    int at[kFftRegElems];
+#pragma unroll
+    for (int q = 0; q < kFftRegElems; ++q) {
+        const int idx = threadIdx.x + q * kFftThreads;
+        v[q] = make_float2(0.f, 0.f);
+        at[q] = -1;
+        if (idx < tot) {
+            int sq, i;
+            if (colmajor) { sq = idx & cm; i = idx >> lc; }
+            else { sq = udiv(idx, n, rn); i = idx - sq * n; }
+            at[q] = sq * lss + i * les;
+            if (sq < cs) {
+                int gs = s0 + sq + sroll, gi = i + iroll;
+                if (gs >= nseq) gs -= nseq;
+                if (gi >= n) gi -= n;
+                v[q] = in[(size_t)gs * in_ss + (size_t)gi * in_es];
+            }
         }
+    }
+#pragma unroll
+    for (int q = 0; q < kFftRegElems; ++q)
+        if (at[q] >= 0) smem[at[q]] = v[q];
+    __syncthreads();
+    int Ns = 1;
+    for (int st = 0; st < pl.nstages; ++st) {
+        const int R = pl.radix[st];
+        switch (R) {
+            case 4: fft_inplace_pass<4, INV>(smem, n, lc, lss, les, Ns, tw); break;
+            case 2: fft_inplace_pass<2, INV>(smem, n, lc, lss, les, Ns, tw); break;
+            case 3: fft_inplace_pass<3, INV>(smem, n, lc, lss, les, Ns, tw); break;
+            default: fft_inplace_pass<5, INV>(smem, n, lc, lss, les, Ns, tw); break;
+        }
+        Ns *= R;
+    }
+    const bool ocol = out_es != 1;
+    for (int idx = threadIdx.x; idx < tot; idx += kFftThreads) {
+        int sq, i;
+        if (ocol) { sq = idx & cm; i = idx >> lc; }
+        else { sq = udiv(idx, n, rn); i = idx - sq * n; }
+        if (sq < cs) out[(size_t)(s0 + sq) * out_ss + (size_t)i * out_es] = cscale(smem[sq * lss + i * les], scale);
     }
 }
 
@@ -286,26 +364,37 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     return hipGetLastError();
 }
 
-int fft_seq_per_block(int n) {
-    // keep 2*C*n*8 bytes <= 64 KiB so several blocks fit per CU
-    int c = (int)(65536 / (16 * (size_t)n));
-    if (c > 16) c = 16;
-    if (c < 1) c = 1;
-    return c;
+// largest C = 2^lc with C*n complex values in registers across the block
+// (kFftRegElems per thread; radix-5 passes hold 20) and at most 16 sequences
+int fft_log2_seq_per_block(const FftPlan &pl) {
+    bool has5 = false;
+    for (int i = 0; i < pl.nstages; ++i) has5 |= pl.radix[i] == 5;
+    const int cap = (has5 ? 20 : kFftRegElems) * kFftThreads;
+    int lc = 0;
+    while (lc < 4 && (pl.n << (lc + 1)) <= cap) ++lc;
+    return (pl.n << lc) <= cap ? lc : -1;
 }
+
+int fft_max_len() { return 20 * kFftThreads; }
 
 hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
                             int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
                             int out_es, int sroll, int iroll, float scale, hipStream_t s) {
-    const int C = fft_seq_per_block(pl.n);
-    const size_t lds = 2 * (size_t)C * pl.n * sizeof(float2);
+    const int lc = fft_log2_seq_per_block(pl);
+    if (lc < 0) return hipErrorInvalidValue;
+    const int C = 1 << lc;
+    // row-major tiles carry one pad element per sequence
+    const size_t lds = (size_t)C * (pl.n + 1) * sizeof(float2);
     dim3 grid((nseq + C - 1) / C, B);
+    hipError_t e = hipFuncSetAttribute(inverse ? (const void *)k_fft_batch<true> : (const void *)k_fft_batch<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
     if (inverse)
-        hipLaunchKernelGGL(k_fft_batch<true>, grid, dim3(256), lds, s, in, out, pl, tw, C, nseq, in_bs, in_ss,
-                           in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
+        hipLaunchKernelGGL(k_fft_batch<true>, grid, dim3(kFftThreads), lds, s, in, out, pl, tw, lc, nseq, in_bs,
+                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
     else
-        hipLaunchKernelGGL(k_fft_batch<false>, grid, dim3(256), lds, s, in, out, pl, tw, C, nseq, in_bs, in_ss,
-                           in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
+        hipLaunchKernelGGL(k_fft_batch<false>, grid, dim3(kFftThreads), lds, s, in, out, pl, tw, lc, nseq, in_bs,
+                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
     return hipGetLastError();
 }
 

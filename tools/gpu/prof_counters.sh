@@ -1,16 +1,15 @@
-# PMC passes on the fused kernel (separate passes, --kernel-trace only alongside --pmc)
+# HBM traffic passes (MI355X_MICROARCH.md "HBM [CDNA4]"): FETCH_SIZE and
+# WRITE_SIZE in separate passes, --kernel-trace only alongside --pmc.
+# k_permute_meas moves a known byte count with the same 2-byte-per-lane reads
+# as the fused kernel's measurement stream and calibrates FETCH_SIZE.
+set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc
 mkdir -p $OUT
-B="python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --data random"
-true
-
 i=0
-for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
-         "SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM" \
-         "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+for P in "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_PMC:-}; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex k_fused --output-format csv -d $OUT/p$i -o run -- $B > $OUT/p$i.log 2>&1 || { echo "pass $i rc=$?"; tail -3 $OUT/p$i.log; }
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex "k_fused|k_permute|k_fft_batch" --output-format csv -d $OUT/p$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/p$i.log 2>&1 || { echo "pass $i rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
-ls -R $OUT | head -40
+python3 tools/pmc_to_json.py $OUT gpurun_out/pmc_latest.json
