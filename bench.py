@@ -184,8 +184,8 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        glist = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
-        dist.gather(mine, glist, dst=0)
+        from fpm_amd import parallel
+        parallel.gather_tiles(mine, dist, dst=0)
         torch.cuda.synchronize()
         gms = (time.perf_counter() - g0) * 1e3
         gather = dict(ms=round(gms, 2), GB_to_rank0=round(mine.numel() * 4 * (world - 1) / 1e9, 3))

@@ -1,31 +1,36 @@
 // fpm_fused.hip -- the fused per-patch FPM iteration for Np = 256 (the metric
-// configuration): ONE launch per runFPM iteration, one 1024-thread workgroup
+// configuration): ONE launch per runFPM iteration, one 512-thread workgroup
 // per patch, walking every LED of the order (fpmMain.cpp:348-476) without
 // leaving the kernel.  Patches never interact, so there is no inter-workgroup
-// communication at all.
+// communication at all; the whole per-LED intermediate lives in LDS.
 //
 // Per LED step, per workgroup (R = naRadius, box = 2R+1 rows, 16-lane groups):
-//   A  gather O = spec[yc+ky][xc+kx] on the support, X = O*P      (:358-364)
-//      row IDFTs of the box rows  -> T (global, L2-resident)     (:365 rows)
-//   B  per column x: column IDFT (only box rows non-zero), 1/Np^2,
-//      psi' = sqrt(I) psi/|psi + eps| (eps on Re), column DFT, keep the box
-//      rows  -> T (in place)                                     (:365-394)
-//   C  row DFTs of the box rows, pruned to the support columns; object
-//      update written to the centred spectrum; pupil numerator  (:394-447,457-464)
-//   D  tile maxima of |spec| under the ROI -> exact max|objF|  (:460,467)
-//      P += num/max * S, max|P| for the next LED                 (:468-475,415)
+//   gather  O = spec[yc+ky][xc+kx] on the support into registers   (:358-362)
+//   for each half h of the columns (x in [128h, 128h+128)):
+//     A  row IDFTs of the box rows of O*P (:364-365), the half's 128
+//        outputs -> LDS half-T (64 FFT rows + <= 8 "tail" rows by direct sums)
+//     B  per column x: column IDFT (only box rows are non-zero), 1/Np^2,
+//        psi' = sqrt(I) psi/|psi + eps| (eps on Re), column DFT, keep the box
+//        rows -> half-T in place                                   (:365-394)
+//     C  row DFTs of the half rows, output-pruned to the support columns,
+//        accumulated over the two halves in registers              (:394)
+//   update  object update into the centred spectrum (:405-447) and pupil
+//           numerator (:457-464); tile maxima of |spec| kept exact
+//           incrementally (atomicMax + dirty bits)
+//   max     exact max|objF| from the tile maxima (:460,467), dirty tiles re-read
+//           only when their bound exceeds the clean maximum
+//   P       P += num/max * S, max|P| for the next LED            (:468-475,415)
 //
 // 256-point transforms are 16x16 four-step DFTs: a 16-lane group holds 16
 // complex values per lane (element index = lane + 16*register), does the two
-// 16-point DFTs in registers and exchanges once through an XOR-swizzled,
-// conflict-free 2 KiB LDS tile.  Every distribution lines up: the row IDFT
-// input, the row DFT output and the pupil/object registers share the
-// "kx = lane + 16*k" layout, so P and the pre-update O never move.  Only
-// k in {0,1,2,13,14,15} (|kx| <= 47) can be inside the support, so inputs of
-// the inverse transforms and outputs of the forward ones are pruned to those
-// six registers.  Box rows beyond the 64 groups ("tail rows", the outermost
-// rows of the disk with a handful of pixels) are transformed by direct DFT
-// sums spread over all threads.
+// 16-point DFTs in registers and exchanges once through a padded (pitch 17),
+// conflict-free LDS tile.  The row IDFT input, the row DFT output and the
+// pupil/object registers share the "kx = lane + 16*k" layout, so P and the
+// pre-update O never move.  Only k in {0,1,2,13,14,15} (|kx| <= 47) can be
+// inside the support, so inputs of the inverse transforms and outputs of the
+// forward ones are pruned to those six registers.  Box rows beyond the 64
+// FFT rows ("tail rows", the outermost rows of the disk with a handful of
+// pixels) are transformed by direct DFT sums spread over all threads.
 #include <hip/hip_runtime.h>
 
 #include <vector>
