@@ -203,23 +203,23 @@ __device__ __forceinline__ void exchange16(float2 *scr, int t, int gb, const flo
 
 // inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six
 // SK registers may be non-zero), output r[m2] = x[t + 16 m2]
-__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const float2 *tw2,
+__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const float2 (&wt)[16],
                                             int t, int gb) {
     float2 y[16];
     dft16_in6<true>(v, y);
 #pragma unroll
-    for (int m1 = 1; m1 < 16; ++m1) y[m1] = cmul(y[m1], cconj(tw2[m1 * 16 + t]));
+    for (int m1 = 1; m1 < 16; ++m1) y[m1] = cmul(y[m1], cconj(wt[m1]));
     exchange16(scr, t, gb, y, v);
     dft16<true>(v, r);
 }
 
 // forward 256-point DFT, input v[n2] = x[t + 16 n2], output o[s] = X[t + 16 SK[s]]
-__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const float2 *tw2,
+__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const float2 (&wt)[16],
                                             int t, int gb) {
     float2 y[16];
     dft16<false>(v, y);
 #pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], tw2[k1 * 16 + t]);
+    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
     exchange16(scr, t, gb, y, v);
     dft16_out6<false>(v, o);
 }
@@ -253,12 +253,12 @@ __device__ __forceinline__ void dft16_inhalf(float2 (&v)[16], float2 (&r)[16]) {
 // forward 256-point DFT of a half row (x = t + 16 n2, n2 in [8H, 8H+8), zero
 // elsewhere), output o[s] = X[t + 16 SK[s]]
 template <int H>
-__device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const float2 *tw2,
-                                                   int t, int gb) {
+__device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr,
+                                                   const float2 (&wt)[16], int t, int gb) {
     float2 y[16];
     dft16_inhalf<false, H>(v, y);
 #pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], tw2[k1 * 16 + t]);
+    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
     exchange16(scr, t, gb, y, v);
     dft16_out6<false>(v, o);
 }
@@ -275,8 +275,8 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
     float2 *scr_all = sm;                           // NG * XTILE: per-group exchange tiles
-    float2 *th = scr_all + NG * XTILE;              // nrows * TLD: half of T = row IDFTs of the box rows
-    float2 *tw2 = th + nrows * TLD;                 // [m1][t] = W256^{m1 t}
+    float2 *th = scr_all + NG * XTILE;              // (nrows + 2) * TLD: half of T = row IDFTs of the box rows
+    float2 *tw2 = th + (nrows + 2) * TLD;           // [m1][t] = W256^{m1 t}  (after the zero + dummy rows)
     float2 *tw = tw2 + 256;                         // W256^k
     float2 *tailX = tw + 256;                       // MAXTAIL
     float2 *tailF = tailX + MAXTAIL;                // MAXTAIL
@@ -340,7 +340,17 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             P[j][s] = in ? pup[(kyr[j] + R) * NB + kx + R] : make_float2(0.f, 0.f);
         }
     }
-    __syncthreads();  // tpx / tky
+    __syncthreads();  // tpx / tky / sig
+    // per-lane half-T row offsets of this lane's six column slots; rows
+    // outside the box read the zero row `nrows` and write the dummy row after it
+    const int zoff = nrows * TLD;
+    int roff[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int sg = sig[slot_kx(t, s) + KYOFF];
+        roff[s] = sg >= 0 ? sg * TLD : zoff;
+    }
+    for (int i = tid; i < TLD; i += NT) th[zoff + i] = make_float2(0.f, 0.f);
     const bool towner = tid < a.n_tail_px;
     const int2 tp = towner ? tpx[tid] : make_int2(0, 0);
     float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
@@ -382,6 +392,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         float2 v[16], r[16];
 #pragma unroll 1
         for (int h = 0; h < 2; ++h) {
+            // this lane's four-step twiddles W256^{m t}, m = 0..15, in registers
+            // for the whole half (a table read per use serialises on LDS latency)
+            float2 wt[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) wt[m] = tw2[m * 16 + t];
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
@@ -390,7 +405,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = cmul(O[j][s], P[j][s]);   // :364
-                idft256_in6(v, r, scr, tw2, t, gb);
+                idft256_in6(v, r, scr, wt, t, gb);
                 float2 *row = th + (g + NG * j) * TLD + t;
                 if (h == 0) {
 #pragma unroll
@@ -435,11 +450,8 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    const int sg = sig[slot_kx(t, s) + KYOFF];
-                    if (sg >= 0) v[SK[s]] = th[sg * TLD + xl];
-                }
-                idft256_in6(v, r, scr, tw2, t, gb);
+                for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + xl];
+                idft256_in6(v, r, scr, wt, t, gb);
                 const unsigned iw[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
@@ -451,12 +463,9 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                     v[m2] = make_float2(psi.x * sc, psi.y * sc);
                 }
                 float2 o[6];
-                dft256_out6(v, o, scr, tw2, t, gb);
+                dft256_out6(v, o, scr, wt, t, gb);
 #pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    const int sg = sig[slot_kx(t, s) + KYOFF];
-                    if (sg >= 0) th[sg * TLD + xl] = o[s];
-                }
+                for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
             }
             __syncthreads();
             FPM_STAMP(2)
@@ -472,11 +481,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 if (h == 0) {
 #pragma unroll
                     for (int m = 0; m < 8; ++m) v[m] = row[16 * m];
-                    dft256_inhalf_out6<0>(v, o, scr, tw2, t, gb);
+                    dft256_inhalf_out6<0>(v, o, scr, wt, t, gb);
                 } else {
 #pragma unroll
                     for (int m = 0; m < 8; ++m) v[8 + m] = row[16 * m];
-                    dft256_inhalf_out6<1>(v, o, scr, tw2, t, gb);
+                    dft256_inhalf_out6<1>(v, o, scr, wt, t, gb);
                 }
 #pragma unroll
                 for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], o[s]);
@@ -698,7 +707,7 @@ FusedGeom fused_geometry(int np, int r) {
 }
 
 size_t fused_lds_bytes(int ntiles, int n_tail_rows) {
-    return (size_t)(fz::NG * XTILE + (fz::NROWS + n_tail_rows) * TLD + 256 + 256 + 2 * fz::MAXTAIL) *
+    return (size_t)(fz::NG * XTILE + (fz::NROWS + n_tail_rows + 2) * TLD + 256 + 256 + 2 * fz::MAXTAIL) *
                sizeof(float2) +
            32 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
            (size_t)ntiles * sizeof(float) + (size_t)(ntiles + 31) / 32 * sizeof(unsigned);
