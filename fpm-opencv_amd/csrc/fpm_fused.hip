@@ -397,6 +397,17 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             float2 wt[16];
 #pragma unroll
             for (int m = 0; m < 16; ++m) wt[m] = tw2[m * 16 + t];
+            // measurement I[t + 16 m2][x] for this lane's first pass-B column,
+            // issued before pass A so the HBM latency hides behind it; later
+            // columns are prefetched one round ahead inside pass B
+            constexpr int NQ = TH / (4 * (NT / 64));
+            auto colx = [&](int q) { const int r8 = w + (NT / 64) * q; return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
+            uint4 n0, n1;
+            {
+                const uint4 *ip = (const uint4 *)(Ib + ((colx(0) + TH * h) * 16 + t) * 16);
+                n0 = ip[0];
+                n1 = ip[1];
+            }
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
@@ -429,15 +440,6 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             FPM_STAMP(1)
 
             // ---- B: columns x in [128h, 128h+128): IDFT, amplitude replacement, DFT (:365-394)
-            constexpr int NQ = TH / (4 * (NT / 64));
-            auto colx = [&](int q) { const int r8 = w + (NT / 64) * q; return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
-            // measurement I[t + 16 m2][x] for this lane, prefetched one round ahead
-            uint4 n0, n1;
-            {
-                const uint4 *ip = (const uint4 *)(Ib + ((colx(0) + TH * h) * 16 + t) * 16);
-                n0 = ip[0];
-                n1 = ip[1];
-            }
 #pragma unroll 1
             for (int q = 0; q < NQ; ++q) {
                 const int xl = colx(q);
