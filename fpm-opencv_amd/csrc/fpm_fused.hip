@@ -263,6 +263,14 @@ __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[
     dft16_out6<false>(v, o);
 }
 
+// measurement stream: read once per LED, so load it non-temporally and keep
+// L2 for the spectrum window the next LED re-reads
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
+    const u32x4_t v = __builtin_nontemporal_load((const u32x4_t *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
 
 // half-row intermediate in LDS: row pitch 129 complex, so the 16 lanes of a
@@ -405,8 +413,8 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             uint4 n0, n1;
             {
                 const uint4 *ip = (const uint4 *)(Ib + ((colx(0) + TH * h) * 16 + t) * 16);
-                n0 = ip[0];
-                n1 = ip[1];
+                n0 = ld_stream(ip);
+                n1 = ld_stream(ip + 1);
             }
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
 #pragma unroll
@@ -446,8 +454,8 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 const uint4 i0 = n0, i1 = n1;
                 if (q + 1 < NQ) {
                     const uint4 *ip = (const uint4 *)(Ib + ((colx(q + 1) + TH * h) * 16 + t) * 16);
-                    n0 = ip[0];
-                    n1 = ip[1];
+                    n0 = ld_stream(ip);
+                    n1 = ld_stream(ip + 1);
                 }
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
