@@ -38,6 +38,9 @@ __device__ __forceinline__ float2 mul_mi(float2 a) {
 // |a|^2 with an explicit fma so every kernel rounds it identically (the fused
 // path compares tile maxima bit for bit with freshly computed magnitudes)
 __device__ __forceinline__ float cabs2(float2 a) { return __builtin_fmaf(a.x, a.x, a.y * a.y); }
+// |a| as stored in the tile maxima: every kernel that writes or compares a
+// tile maximum uses this one function (raw v_sqrt_f32, no denormal fix-up)
+__device__ __forceinline__ float cmag(float2 a) { return __builtin_amdgcn_sqrtf(cabs2(a)); }
 
 template <bool INV>
 __device__ __forceinline__ void dft2(float2 *v) {

@@ -271,6 +271,8 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+constexpr int RPG_SLOTS = fz::RPG * 6;  // F values per lane
+
 __device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
 
 // half-row intermediate in LDS: row pitch 129 complex, so the 16 lanes of a
@@ -333,7 +335,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     float2 *pup = st.pupil + (size_t)b * NB * NB;
     int kyr[RPG];
     bool ron[RPG];
-    float2 P[RPG][6], O[RPG][6], F[RPG][6];
+    float2 P[RPG][6];
+    // partial row-DFT outputs (Objfup on the box) of this lane, staged in
+    // global scratch between the two column halves so no register holds them
+    // through pass B: [slot][NT] per patch, coalesced
+    float2 *Fs = st.T + (size_t)b * NT * RPG_SLOTS + tid;
     unsigned inmask[RPG];
 #pragma unroll
     for (int j = 0; j < RPG; ++j) {
@@ -376,6 +382,25 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         acc[i] += now_ - prev;                                        \
         prev = now_;                                                  \
     }
+    // O (pre-update Objfcrop on the support, fpmMain.cpp:358-362) is never
+    // held in registers through pass B: Opre is loaded at the start of pass C
+    // for the second half's pass A and the object update, and right after the
+    // object update for the next LED's first pass A.
+    auto window = [&](int itn) {
+        const int ln = a.order[itn];
+        return spec + (unsigned)((a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2);
+    };
+    auto ldO = [&](const float2 *sr, int j, int s) {
+        return ((inmask[j] >> s) & 1) ? sr[kyr[j] * L + slot_kx(t, s)] : make_float2(0.f, 0.f);
+    };
+    float2 Opre[RPG][6];
+    if (a.n_order > 0) {
+        const float2 *sr = window(0);
+#pragma unroll
+        for (int j = 0; j < RPG; ++j)
+#pragma unroll
+            for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(sr, j, s);
+    }
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
@@ -383,13 +408,6 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         const uint16_t *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
 
         // ---- gather the sub-aperture on the support (pre-update Objfcrop, fpmMain.cpp:358-362)
-#pragma unroll
-        for (int j = 0; j < RPG; ++j)
-#pragma unroll
-            for (int s = 0; s < 6; ++s) {
-                O[j][s] = ((inmask[j] >> s) & 1) ? srow[kyr[j] * L + slot_kx(t, s)] : make_float2(0.f, 0.f);
-                F[j][s] = make_float2(0.f, 0.f);
-            }
         if (towner) {
             Ot = srow[tp.x * L + tp.y];
             tailX[tid] = cmul(Ot, Pt);
@@ -398,6 +416,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         FPM_STAMP(0)
 
         float2 v[16], r[16];
+        float2 F[RPG][6];  // row-DFT outputs; complete after the second half
 #pragma unroll 1
         for (int h = 0; h < 2; ++h) {
             // this lane's four-step twiddles W256^{m t}, m = 0..15, in registers
@@ -417,13 +436,18 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 n1 = ld_stream(ip + 1);
             }
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
+            float2 X[RPG][6];
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) X[j][s] = cmul(Opre[j][s], P[j][s]);   // :364
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
                 if (!ron[j]) continue;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-                for (int s = 0; s < 6; ++s) v[SK[s]] = cmul(O[j][s], P[j][s]);   // :364
+                for (int s = 0; s < 6; ++s) v[SK[s]] = X[j][s];
                 idft256_in6(v, r, scr, wt, t, gb);
                 float2 *row = th + (g + NG * j) * TLD + t;
                 if (h == 0) {
@@ -481,9 +505,21 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             FPM_STAMP(2)
 
             // ---- C: this half's share of the pruned row DFTs (:394)
+            float2 Fp[RPG][6];
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) {
+                    Opre[j][s] = ldO(srow, j, s);
+                    Fp[j][s] = h ? Fs[(j * 6 + s) * NT] : make_float2(0.f, 0.f);
+                }
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
-                if (!ron[j]) continue;
+                if (!ron[j]) {
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) F[j][s] = make_float2(0.f, 0.f);
+                    continue;
+                }
                 const float2 *row = th + (g + NG * j) * TLD + t;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
@@ -498,7 +534,10 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                     dft256_inhalf_out6<1>(v, o, scr, wt, t, gb);
                 }
 #pragma unroll
-                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], o[s]);
+                for (int s = 0; s < 6; ++s) {
+                    F[j][s] = cadd(Fp[j][s], o[s]);
+                    if (h == 0) Fs[(j * 6 + s) * NT] = F[j][s];
+                }
             }
             for (int pp = g; pp < a.n_tail_px; pp += NG) {  // tail pixels: 16 lanes sum 128 terms
                 const int2 px = tpx[pp];
@@ -530,37 +569,48 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             if (an < ao && tmu[ti] <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
             atomicMax(&tmu[ti], __float_as_uint(an));
         };
+        // Straight-line over all slots: outside the support O = P = 0, so the
+        // numerator is exactly 0 and only the spectrum store and the tile
+        // bookkeeping need the mask.
 #pragma unroll
         for (int j = 0; j < RPG; ++j)
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                if (!((inmask[j] >> s) & 1)) continue;
                 const int kx = slot_kx(t, s);
-                const float2 p = P[j][s], o = O[j][s];
+                const float2 p = P[j][s], o = Opre[j][s];
                 const float2 D = csub(F[j][s], cmul(o, p));   // Objfup - ObjfcropP (:409)
-                const float pa = sqrtf(cabs2(p));
+                const float pa = cmag(p);
                 const float rin = __builtin_amdgcn_rcpf((pa * pa + st.delta2) * pm);
                 const float2 nv = cadd(o, cscale(cmul(D, cscale(cconj(p), pa)), rin));
-                srow[kyr[j] * L + kx] = nv;
-                const float oa = sqrtf(cabs2(o));
+                const float oa = cmag(o);
                 const float rip = __builtin_amdgcn_rcpf(oa * oa + st.delta1);
                 // this group's own half-T row is no longer read: park the numerator there
                 th[(g + NG * j) * TLD + s * 16 + t] = cscale(cmul(D, cscale(cconj(o), oa)), rip);
-                note(yc + kyr[j], xc + kx, oa, sqrtf(cabs2(nv)));
+                if ((inmask[j] >> s) & 1) {
+                    srow[kyr[j] * L + kx] = nv;
+                    note(yc + kyr[j], xc + kx, oa, cmag(nv));
+                }
             }
         if (towner) {
             const float2 p = Pt, o = Ot;
             const float2 D = csub(tailF[tid], tailX[tid]);
-            const float pa = sqrtf(cabs2(p));
+            const float pa = cmag(p);
             const float rin = __builtin_amdgcn_rcpf((pa * pa + st.delta2) * pm);
             const float2 nv = cadd(o, cscale(cmul(D, cscale(cconj(p), pa)), rin));
             srow[tp.x * L + tp.y] = nv;
-            const float oa = sqrtf(cabs2(o));
+            const float oa = cmag(o);
             const float rip = __builtin_amdgcn_rcpf(oa * oa + st.delta1);
             NPt = cscale(cmul(D, cscale(cconj(o), oa)), rip);
-            note(yc + tp.x, xc + tp.y, oa, sqrtf(cabs2(nv)));
+            note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
         __syncthreads();  // spectrum writes, tile maxima, dirty bits
+        if (it + 1 < a.n_order) {
+            const float2 *sr = window(it + 1);
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(sr, j, s);
+        }
         FPM_STAMP(4)
 
         // ---- exact max|objF| (:460,467): max over clean tiles; dirty tiles
@@ -594,11 +644,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int pp = lane + 64 * jj;
-                    mm = fmaxf(mm, cabs2(spec[(unsigned)((ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15))]));
+                    mm = fmaxf(mm, cmag(spec[(unsigned)((ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15))]));
                 }
                 mm = wave_max(mm);
                 if (lane == 0) {
-                    tmx[i] = sqrtf(mm);
+                    tmx[i] = mm;
                     atomicAnd(&dirty[i >> 5], ~(1u << (i & 31)));
                 }
             }
@@ -622,7 +672,6 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         for (int j = 0; j < RPG; ++j)
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                if (!((inmask[j] >> s) & 1)) continue;
                 const float2 n = th[(g + NG * j) * TLD + s * 16 + t];
                 P[j][s] = make_float2(P[j][s].x + n.x * rom, P[j][s].y + n.y * rom);
                 pmx = fmaxf(pmx, cabs2(P[j][s]));
@@ -730,7 +779,9 @@ bool fused_supported(int np, int r, int L) {
     return g.ok && (L % kTile == 0) && fused_lds_bytes(ntiles, g.n_tail_rows) <= 160 * 1024;
 }
 
-size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
+// the intermediate T lives in LDS; the global scratch only carries each
+// lane's partial row-DFT outputs F from the first column half to the second
+size_t fused_T_elems(int, int, int B) { return (size_t)B * fz::NT * RPG_SLOTS; }
 
 size_t fused_meas_bytes(int np, int B, int n_stack) { return (size_t)n_stack * B * np * np * sizeof(uint16_t); }
 

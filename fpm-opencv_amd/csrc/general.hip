@@ -114,12 +114,12 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
         const float2 F = res[(kx + np) % np];    // Objfup (:394)
         const float2 D = csub(F, cmul(o, p));    // Objfup - ObjfcropP (:409,463)
         // object update (:406-419,433): D |P| P* / ((|P|^2 + d2) max|P|)
-        const float pa = sqrtf(cabs2(p));
+        const float pa = cmag(p);
         const float den_o = (pa * pa + st.delta2) * pm;
         const float2 dpc = cmul(D, cscale(cconj(p), pa));
         spec[si] = make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o);
         // pupil numerator (:459-464,469): D |O| O* / (|O|^2 + d1); max|objF| in K4
-        const float oa = sqrtf(cabs2(o));
+        const float oa = cmag(o);
         const float den_p = oa * oa + st.delta1;
         const float2 n = cmul(D, cscale(cconj(o), oa));
         dP[row * nb + j] = make_float2(n.x / den_p, n.y / den_p);
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
             ty = ty0 + t / ntw;
             tx = tx0 + t % ntw;
             const int y = ty * kTile + (qt >> 4), x = tx * kTile + (qt & 15);
-            if (y < L && x < L) m = sqrtf(cabs2(spec[(size_t)y * L + x]));
+            if (y < L && x < L) m = cmag(spec[(size_t)y * L + x]);
         }
         m = wave_max(m);
         if (lane == 0) tred[q][wq] = m;
@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
         p.x += d.x / omax;
         p.y += d.y / omax;
         pup[i] = p;
-        pm = fmaxf(pm, sqrtf(cabs2(p)));
+        pm = fmaxf(pm, cmag(p));
     }
     pm = block_max(pm, red);
     if (threadIdx.x == 0) st.pmax[b] = pm;
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
     const int ty = t / st.ntx, tx = t % st.ntx;
     const int y = ty * kTile + (threadIdx.x >> 4), x = tx * kTile + (threadIdx.x & 15);
     float m = 0.f;
-    if (y < L && x < L) m = sqrtf(cabs2(st.spec[(size_t)b * L * L + (size_t)y * L + x]));
+    if (y < L && x < L) m = cmag(st.spec[(size_t)b * L * L + (size_t)y * L + x]);
     m = block_max(m, red);
     if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = m;
 }
