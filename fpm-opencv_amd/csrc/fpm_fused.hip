@@ -271,8 +271,6 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-constexpr int RPG_SLOTS = fz::RPG * 6;  // F values per lane
-
 __device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
 
 // half-row intermediate in LDS: row pitch 129 complex, so the 16 lanes of a
@@ -336,10 +334,6 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     int kyr[RPG];
     bool ron[RPG];
     float2 P[RPG][6];
-    // partial row-DFT outputs (Objfup on the box) of this lane, staged in
-    // global scratch between the two column halves so no register holds them
-    // through pass B: [slot][NT] per patch, coalesced
-    float2 *Fs = st.T + (size_t)b * NT * RPG_SLOTS + tid;
     unsigned inmask[RPG];
 #pragma unroll
     for (int j = 0; j < RPG; ++j) {
@@ -511,7 +505,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int s = 0; s < 6; ++s) {
                     Opre[j][s] = ldO(srow, j, s);
-                    Fp[j][s] = h ? Fs[(j * 6 + s) * NT] : make_float2(0.f, 0.f);
+                    Fp[j][s] = h ? F[j][s] : make_float2(0.f, 0.f);
                 }
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
@@ -536,7 +530,6 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int s = 0; s < 6; ++s) {
                     F[j][s] = cadd(Fp[j][s], o[s]);
-                    if (h == 0) Fs[(j * 6 + s) * NT] = F[j][s];
                 }
             }
             for (int pp = g; pp < a.n_tail_px; pp += NG) {  // tail pixels: 16 lanes sum 128 terms
@@ -779,9 +772,7 @@ bool fused_supported(int np, int r, int L) {
     return g.ok && (L % kTile == 0) && fused_lds_bytes(ntiles, g.n_tail_rows) <= 160 * 1024;
 }
 
-// the intermediate T lives in LDS; the global scratch only carries each
-// lane's partial row-DFT outputs F from the first column half to the second
-size_t fused_T_elems(int, int, int B) { return (size_t)B * fz::NT * RPG_SLOTS; }
+size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
 size_t fused_meas_bytes(int np, int B, int n_stack) { return (size_t)n_stack * B * np * np * sizeof(uint16_t); }
 
