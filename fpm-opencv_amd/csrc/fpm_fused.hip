@@ -185,42 +185,46 @@ __device__ __forceinline__ void dft16_out6(float2 (&v)[16], float2 (&o)[6]) {
 // write (16 lanes, one row) and the read (32 lanes = two groups 2176 B apart)
 // are bank-conflict free, and every access is one base register plus an
 // immediate offset (an XOR swizzle would need 32 per-lane address registers).
+//
+// Ordering: LDS instructions of one wave execute in issue order, so the reads
+// see every lane's writes as long as the COMPILER keeps them in program
+// order.  Alias analysis could otherwise prove that read j only overlaps
+// this lane's own write j (17*m1 + t == 17*t + j needs m1 == j) and hoist the
+// others, so the read base `xrd` (= t*XP) is laundered through an empty asm
+// once per kernel: every read may alias every write and stays after them,
+// while unrelated loads and stores remain free to move across the exchange
+// (a wave_barrier/fence pair here pinned them and cost 7% of the kernel).
 constexpr int XP = 17;                      // exchange-tile row pitch
 constexpr int XTILE = 16 * XP;              // complex per group tile
-__device__ __forceinline__ void exchange16(float2 *scr, int t, int gb, const float2 (&y)[16], float2 (&z)[16]) {
-    (void)gb;
+__device__ __forceinline__ int opaque_int(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
 #pragma unroll
     for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int j = 0; j < 16; ++j) z[j] = scr[t * XP + j];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = 0; j < 16; ++j) z[j] = scr[xrd + j];
 }
 
 // inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six
 // SK registers may be non-zero), output r[m2] = x[t + 16 m2]
-__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const float2 (&wt)[16],
-                                            int t, int gb) {
+__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const float2 (&wt)[16], int t, int xrd) {
     float2 y[16];
     dft16_in6<true>(v, y);
 #pragma unroll
     for (int m1 = 1; m1 < 16; ++m1) y[m1] = cmul(y[m1], cconj(wt[m1]));
-    exchange16(scr, t, gb, y, v);
+    exchange16(scr, t, xrd, y, v);
     dft16<true>(v, r);
 }
 
 // forward 256-point DFT, input v[n2] = x[t + 16 n2], output o[s] = X[t + 16 SK[s]]
-__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const float2 (&wt)[16],
-                                            int t, int gb) {
+__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const float2 (&wt)[16], int t, int xrd) {
     float2 y[16];
     dft16<false>(v, y);
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
-    exchange16(scr, t, gb, y, v);
+    exchange16(scr, t, xrd, y, v);
     dft16_out6<false>(v, o);
 }
 
@@ -254,12 +258,12 @@ __device__ __forceinline__ void dft16_inhalf(float2 (&v)[16], float2 (&r)[16]) {
 // elsewhere), output o[s] = X[t + 16 SK[s]]
 template <int H>
 __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr,
-                                                   const float2 (&wt)[16], int t, int gb) {
+                                                   const float2 (&wt)[16], int t, int xrd) {
     float2 y[16];
     dft16_inhalf<false, H>(v, y);
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
-    exchange16(scr, t, gb, y, v);
+    exchange16(scr, t, xrd, y, v);
     dft16_out6<false>(v, o);
 }
 
@@ -296,7 +300,8 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     unsigned *dirty = (unsigned *)(tmx + a.ntiles); // ntiles bits: tile max may be stale-high
 
     const DevState &st = a.st;
-    const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gb = g & 1, gg = (tid >> 4) & 3;
+    const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
+    const int xrd = opaque_int(t * XP);  // exchange read base, see exchange16
     const int lane = tid & 63, w = tid >> 6;
     const int b = blockIdx.x;
     const int R = st.r, NB = st.nb, L = st.L;
@@ -442,7 +447,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = X[j][s];
-                idft256_in6(v, r, scr, wt, t, gb);
+                idft256_in6(v, r, scr, wt, t, xrd);
                 float2 *row = th + (g + NG * j) * TLD + t;
                 if (h == 0) {
 #pragma unroll
@@ -479,7 +484,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + xl];
-                idft256_in6(v, r, scr, wt, t, gb);
+                idft256_in6(v, r, scr, wt, t, xrd);
                 const unsigned iw[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
@@ -491,7 +496,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                     v[m2] = make_float2(psi.x * sc, psi.y * sc);
                 }
                 float2 o[6];
-                dft256_out6(v, o, scr, wt, t, gb);
+                dft256_out6(v, o, scr, wt, t, xrd);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
             }
@@ -521,11 +526,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 if (h == 0) {
 #pragma unroll
                     for (int m = 0; m < 8; ++m) v[m] = row[16 * m];
-                    dft256_inhalf_out6<0>(v, o, scr, wt, t, gb);
+                    dft256_inhalf_out6<0>(v, o, scr, wt, t, xrd);
                 } else {
 #pragma unroll
                     for (int m = 0; m < 8; ++m) v[8 + m] = row[16 * m];
-                    dft256_inhalf_out6<1>(v, o, scr, wt, t, gb);
+                    dft256_inhalf_out6<1>(v, o, scr, wt, t, xrd);
                 }
 #pragma unroll
                 for (int s = 0; s < 6; ++s) {
