@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
     float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
     float pm = st.pmax[b];
-    const float inv_n2 = 1.0f / (float)(NP * NP);
+    const float epsn = st.eps * (float)(NP * NP);  // eps on the unscaled IDFT
     __syncthreads();
 
     // diagnostic: shader-clock cycles per phase, summed over LEDs (wave-uniform)
@@ -475,8 +475,10 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             for (int q = 0; q < NQ; ++q) {
                 const int xl = colx(q);
                 const uint4 i0 = n0, i1 = n1;
-                if (q + 1 < NQ) {
-                    const uint4 *ip = (const uint4 *)(Ib + ((colx(q + 1) + TH * h) * 16 + t) * 16);
+                {   // unconditional (the last round re-reads its own column) so
+                    // the load is not sunk into a branch at the loop latch
+                    const int qn = q + 1 < NQ ? q + 1 : q;
+                    const uint4 *ip = (const uint4 *)(Ib + ((colx(qn) + TH * h) * 16 + t) * 16);
                     n0 = ld_stream(ip);
                     n1 = ld_stream(ip + 1);
                 }
@@ -489,11 +491,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
                     const float I = (float)((iw[m2 >> 1] >> (16 * (m2 & 1))) & 0xFFFFu);
-                    const float2 psi = cscale(r[m2], inv_n2);
-                    const float tre = psi.x + st.eps;
-                    const float mag2 = tre * tre + psi.y * psi.y;
+                    // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = sqrt(I) r/|r + eps Np^2|
+                    const float tre = r[m2].x + epsn;
+                    const float mag2 = __builtin_fmaf(tre, tre, r[m2].y * r[m2].y);
                     const float sc = __builtin_amdgcn_sqrtf(I) * __builtin_amdgcn_rsqf(mag2);
-                    v[m2] = make_float2(psi.x * sc, psi.y * sc);
+                    v[m2] = make_float2(r[m2].x * sc, r[m2].y * sc);
                 }
                 float2 o[6];
                 dft256_out6(v, o, scr, wt, t, xrd);
