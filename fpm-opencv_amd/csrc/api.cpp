@@ -33,8 +33,8 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
                           hipStream_t s);
 // fused path (fpm_fused.hip)
 bool fused_supported(int np, int r, int L);
-hipError_t fused_permute(const uint16_t *meas, uint16_t *meas_perm, int n_stack, int B, hipStream_t s);
-hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas_perm, const int *order_dev,
+hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s);
+hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   unsigned long long *dbg, hipStream_t s);
 size_t fused_meas_bytes(int np, int B, int n_stack);
@@ -101,7 +101,7 @@ struct fpm_ctx {
     float2 *tw_np = nullptr, *tw_L = nullptr;
     float2 *objcrop = nullptr;
     uint16_t *meas = nullptr;
-    uint16_t *meas_perm = nullptr;  // fused-path layout
+    float *meas_perm = nullptr;     // fused-path layout (reciprocal intensities)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -256,7 +256,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
     } else {
-        if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(uint16_t))))
+        if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(float))))
             return fail(rc);
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
     }

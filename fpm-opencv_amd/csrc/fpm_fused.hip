@@ -54,7 +54,7 @@ constexpr int KYOFF = 48;                     // sigma table covers ky in [-48, 
 
 struct FusedArgs {
     DevState st;
-    const uint16_t *meas_perm;  // [nS][B][x][t][m2]: I[t + 16 m2][x]
+    const float *meas_perm;     // [nS][B][x][t][m2]: 1/I[t + 16 m2][x] (+inf where I = 0)
     const int *order, *x0, *y0;
     const float2 *tw;           // exp(-2 pi i k / 256), k < 256
     int n_order;
@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
         float2 *srow = spec + (unsigned)(yc * L + xc);   // spec[yc + ky][xc + kx] = srow[ky*L + kx]
-        const uint16_t *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
+        const float *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
 
         // ---- gather the sub-aperture on the support (pre-update Objfcrop, fpmMain.cpp:358-362)
         if (towner) {
@@ -428,11 +428,13 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             // columns are prefetched one round ahead inside pass B
             constexpr int NQ = TH / (4 * (NT / 64));
             auto colx = [&](int q) { const int r8 = w + (NT / 64) * q; return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
-            uint4 n0, n1;
+            uint4 n0, n1, n2, n3;
             {
                 const uint4 *ip = (const uint4 *)(Ib + ((colx(0) + TH * h) * 16 + t) * 16);
                 n0 = ld_stream(ip);
                 n1 = ld_stream(ip + 1);
+                n2 = ld_stream(ip + 2);
+                n3 = ld_stream(ip + 3);
             }
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
             float2 X[RPG][6];
@@ -474,27 +476,30 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll 1
             for (int q = 0; q < NQ; ++q) {
                 const int xl = colx(q);
-                const uint4 i0 = n0, i1 = n1;
+                const uint4 i0 = n0, i1 = n1, i2 = n2, i3 = n3;
                 {   // unconditional (the last round re-reads its own column) so
                     // the load is not sunk into a branch at the loop latch
                     const int qn = q + 1 < NQ ? q + 1 : q;
                     const uint4 *ip = (const uint4 *)(Ib + ((colx(qn) + TH * h) * 16 + t) * 16);
                     n0 = ld_stream(ip);
                     n1 = ld_stream(ip + 1);
+                    n2 = ld_stream(ip + 2);
+                    n3 = ld_stream(ip + 3);
                 }
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + xl];
                 idft256_in6(v, r, scr, wt, t, xrd);
-                const unsigned iw[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+                const unsigned iw[16] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w,
+                                         i2.x, i2.y, i2.z, i2.w, i3.x, i3.y, i3.z, i3.w};
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
-                    const float I = (float)((iw[m2 >> 1] >> (16 * (m2 & 1))) & 0xFFFFu);
-                    // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = sqrt(I) r/|r + eps Np^2|
+                    const float invI = __uint_as_float(iw[m2]);
+                    // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
                     const float tre = r[m2].x + epsn;
                     const float mag2 = __builtin_fmaf(tre, tre, r[m2].y * r[m2].y);
-                    const float sc = __builtin_amdgcn_sqrtf(I) * __builtin_amdgcn_rsqf(mag2);
+                    const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
                     v[m2] = make_float2(r[m2].x * sc, r[m2].y * sc);
                 }
                 float2 o[6];
@@ -707,19 +712,20 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     if (tid == 0) st.pmax[b] = pm;
 }
 
-// measurement permutation for coalesced column reads:
-// out[s][b][x][t][m2] = in[s][b][t + 16 m2][x]
+// measurement permutation for coalesced column reads, stored as the
+// reciprocal intensity so amplitude replacement is one rsq per pixel:
+// out[s][b][x][t][m2] = 1 / in[s][b][t + 16 m2][x]   (1/0 = +inf: rsq -> 0)
 // One block transposes a 256(y) x 64(x) slab through LDS: coalesced 128-byte
 // row reads, then each output row x (256 contiguous values) is written by
 // consecutive threads.  grid (NP/64, nimg), block 256.
-__global__ void __launch_bounds__(256) k_permute_meas(const uint16_t *__restrict__ in, uint16_t *__restrict__ out,
+__global__ void __launch_bounds__(256) k_permute_meas(const uint16_t *__restrict__ in, float *__restrict__ out,
                                                       size_t nimg) {
     __shared__ uint16_t tile[fz::NP][64 + 2];
     const size_t img = blockIdx.y;
     if (img >= nimg) return;
     const int xs = blockIdx.x * 64;
     const uint16_t *src = in + img * fz::NP * fz::NP;
-    uint16_t *dst = out + img * fz::NP * fz::NP;
+    float *dst = out + img * fz::NP * fz::NP;
     for (int i = threadIdx.x; i < fz::NP * 64; i += 256) {
         const int y = i >> 6, x = i & 63;
         tile[y][x] = src[(size_t)y * fz::NP + xs + x];
@@ -728,7 +734,7 @@ __global__ void __launch_bounds__(256) k_permute_meas(const uint16_t *__restrict
     for (int i = threadIdx.x; i < 64 * fz::NP; i += 256) {
         const int x = i >> 8, j = i & 255;
         const int y = (j >> 4) + 16 * (j & 15);
-        dst[(size_t)(xs + x) * fz::NP + j] = tile[y][x];
+        dst[(size_t)(xs + x) * fz::NP + j] = 1.0f / (float)tile[y][x];
     }
 }
 
@@ -781,9 +787,9 @@ bool fused_supported(int np, int r, int L) {
 
 size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
-size_t fused_meas_bytes(int np, int B, int n_stack) { return (size_t)n_stack * B * np * np * sizeof(uint16_t); }
+size_t fused_meas_bytes(int np, int B, int n_stack) { return (size_t)n_stack * B * np * np * sizeof(float); }
 
-hipError_t fused_permute(const uint16_t *meas, uint16_t *meas_perm, int n_stack, int B, hipStream_t s) {
+hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s) {
     const size_t nimg = (size_t)n_stack * B;
     for (size_t i0 = 0; i0 < nimg; i0 += 65535) {
         const size_t n = (nimg - i0 < 65535) ? nimg - i0 : 65535;
@@ -793,7 +799,7 @@ hipError_t fused_permute(const uint16_t *meas, uint16_t *meas_perm, int n_stack,
     return hipGetLastError();
 }
 
-hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas_perm, const int *order_dev,
+hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   unsigned long long *dbg, hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
