@@ -264,6 +264,10 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
     in += (size_t)b * in_bs;
     out += (size_t)b * out_bs;
     const int tot = n << lc;
+    // twiddle table in LDS after the tile (a global read per butterfly put an
+    // L1 round trip on every pass's critical path)
+    float2 *stw = smem + (size_t)C * (n + 1);
+    for (int i = threadIdx.x; i < n; i += kFftThreads) stw[i] = tw[i];
     // all of a thread's loads are issued before any LDS store so their
     // latencies overlap (a rolled loop waits for each one in turn)
     float2 v[kFftRegElems];
@@ -294,10 +298,10 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
-            case 4: fft_inplace_pass<4, INV>(smem, n, lc, lss, les, Ns, tw); break;
-            case 2: fft_inplace_pass<2, INV>(smem, n, lc, lss, les, Ns, tw); break;
-            case 3: fft_inplace_pass<3, INV>(smem, n, lc, lss, les, Ns, tw); break;
-            default: fft_inplace_pass<5, INV>(smem, n, lc, lss, les, Ns, tw); break;
+            case 4: fft_inplace_pass<4, INV>(smem, n, lc, lss, les, Ns, stw); break;
+            case 2: fft_inplace_pass<2, INV>(smem, n, lc, lss, les, Ns, stw); break;
+            case 3: fft_inplace_pass<3, INV>(smem, n, lc, lss, les, Ns, stw); break;
+            default: fft_inplace_pass<5, INV>(smem, n, lc, lss, les, Ns, stw); break;
         }
         Ns *= R;
     }
@@ -384,7 +388,7 @@ hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const F
     if (lc < 0) return hipErrorInvalidValue;
     const int C = 1 << lc;
     // row-major tiles carry one pad element per sequence
-    const size_t lds = (size_t)C * (pl.n + 1) * sizeof(float2);
+    const size_t lds = ((size_t)C * (pl.n + 1) + pl.n) * sizeof(float2);  // tile + twiddles
     dim3 grid((nseq + C - 1) / C, B);
     hipError_t e = hipFuncSetAttribute(inverse ? (const void *)k_fft_batch<true> : (const void *)k_fft_batch<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
