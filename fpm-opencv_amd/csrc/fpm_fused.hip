@@ -35,6 +35,7 @@
 
 #include <vector>
 
+#include "dft16.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
 
@@ -66,62 +67,6 @@ struct FusedArgs {
     int ntiles, nwords;         // tiles of |spec| maxima, 32-bit words of the dirty bitmap
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
 };
-
-// ---------------------------------------------------------------- 16-pt DFTs
-// W16^j for the forward transform; the inverse uses the conjugate.
-template <bool INV>
-__device__ __forceinline__ float2 w16(float2 a, int j) {
-    constexpr float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f, R2 = 0.70710678118654752440f;
-    float c, s;  // W16^j = c - i s (forward)
-    switch (j & 15) {
-        case 1: c = C1; s = S1; break;
-        case 2: c = R2; s = R2; break;
-        case 3: c = S1; s = C1; break;
-        case 6: c = -R2; s = R2; break;
-        case 9: c = -C1; s = -S1; break;
-        default: c = 1.f; s = 0.f; break;
-    }
-    if (j == 4) return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
-    const float si = INV ? -s : s;
-    // (a.x + i a.y)(c - i si)
-    return make_float2(a.x * c + a.y * si, a.y * c - a.x * si);
-}
-
-template <bool INV>
-__device__ __forceinline__ void bf4(float2 &a0, float2 &a1, float2 &a2, float2 &a3) {
-    float2 q[4] = {a0, a1, a2, a3};
-    dft4<INV>(q);
-    a0 = q[0];
-    a1 = q[1];
-    a2 = q[2];
-    a3 = q[3];
-}
-
-// twiddles between the two radix-4 stages: position k1 + 4 m1 *= W16^{k1 m1}
-template <bool INV>
-__device__ __forceinline__ void mid_tw(float2 (&v)[16]) {
-    v[5] = w16<INV>(v[5], 1);
-    v[6] = w16<INV>(v[6], 2);
-    v[7] = w16<INV>(v[7], 3);
-    v[9] = w16<INV>(v[9], 2);
-    v[10] = w16<INV>(v[10], 4);
-    v[11] = w16<INV>(v[11], 6);
-    v[13] = w16<INV>(v[13], 3);
-    v[14] = w16<INV>(v[14], 6);
-    v[15] = w16<INV>(v[15], 9);
-}
-
-// dense 16-point DFT: in v[k], out r[m] = sum_k v[k] W16^{+-km}
-template <bool INV>
-__device__ __forceinline__ void dft16(float2 (&v)[16], float2 (&r)[16]) {
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) bf4<INV>(v[k1], v[k1 + 4], v[k1 + 8], v[k1 + 12]);
-    mid_tw<INV>(v);
-#pragma unroll
-    for (int m1 = 0; m1 < 4; ++m1) bf4<INV>(v[4 * m1], v[4 * m1 + 1], v[4 * m1 + 2], v[4 * m1 + 3]);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
-}
 
 // 16-point DFT whose input is zero except v[0,1,2,13,14,15]
 template <bool INV>
@@ -177,34 +122,6 @@ __device__ __forceinline__ void dft16_out6(float2 (&v)[16], float2 (&o)[6]) {
     o[3] = y3(v[4], v[5], v[6], v[7]);                 // m = 13 (m1 1, m2 3)
     o[4] = y3(v[8], v[9], v[10], v[11]);               // m = 14
     o[5] = y3(v[12], v[13], v[14], v[15]);             // m = 15
-}
-
-// ------------------------------------------------------- four-step exchange
-// Lane t of a 16-lane group holds y[m1] (m1 = 0..15); afterwards lane t holds
-// z[j] = y_of_lane_j[t].  The 16x16 tile has a row pitch of 17 complex: the
-// write (16 lanes, one row) and the read (32 lanes = two groups 2176 B apart)
-// are bank-conflict free, and every access is one base register plus an
-// immediate offset (an XOR swizzle would need 32 per-lane address registers).
-//
-// Ordering: LDS instructions of one wave execute in issue order, so the reads
-// see every lane's writes as long as the COMPILER keeps them in program
-// order.  Alias analysis could otherwise prove that read j only overlaps
-// this lane's own write j (17*m1 + t == 17*t + j needs m1 == j) and hoist the
-// others, so the read base `xrd` (= t*XP) is laundered through an empty asm
-// once per kernel: every read may alias every write and stays after them,
-// while unrelated loads and stores remain free to move across the exchange
-// (a wave_barrier/fence pair here pinned them and cost 7% of the kernel).
-constexpr int XP = 17;                      // exchange-tile row pitch
-constexpr int XTILE = 16 * XP;              // complex per group tile
-__device__ __forceinline__ int opaque_int(int v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-__device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
-#pragma unroll
-    for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) z[j] = scr[xrd + j];
 }
 
 // inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six

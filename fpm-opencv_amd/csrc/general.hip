@@ -424,8 +424,13 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
 
 // objCrop = IDFT(objF)/L^2 with objF = fftShift(spec) (fpmMain.cpp:481):
 // rows of the rolled spectrum, then columns, scaled by 1/L^2.
+hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s);
+
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
                           hipStream_t s) {
+    // L = 512 / 768 / 1024: register-resident transforms (objcrop.hip)
+    const hipError_t r = launch_objcrop_regs(st, out, tw_L, s);
+    if (r != hipErrorNotSupported) return r;
     const int L = st.L;
     const size_t bs = (size_t)L * L;
     hipError_t e = launch_fft_batch(true, st.spec, out, pl_L, tw_L, L, st.B, bs, L, 1, bs, L, 1, L / 2, L / 2, 1.f,

@@ -1,0 +1,215 @@
+// objcrop.hip -- objCrop = IDFT2(objF) / L^2 every iteration (fpmMain.cpp:481)
+// for L = 256*M, M in {2, 3, 4} (the fused path's L = Np * resImprovementFactor
+// with Np = 256).  objF = fftShift(spec), spec being the centred spectrum the
+// solver stores (fpm_state.hpp).
+//
+// One L-point transform per 16-lane group, entirely in registers:
+//   x[i], i = M*m + c  (c < M, m < 256):  Y_c = DFT256(x[M*m + c])      (M four-step 256s)
+//   X[k' + 256 p] = sum_c W_L^{c k'} W_M^{c p} Y_c[k']                  (radix-M combine)
+// Lane t holds, for every c, the sub-sequence elements m = t + 16 j (j < 16);
+// after each 256-point four-step it holds Y_c[t + 16 r] (r < 16), so the
+// radix-M combine is lane-local.  The fftShift of objF is free: rolling the
+// row index is a different source row, rolling the element index by L/2 =
+// 8*16*M is the register relabel j -> j + 8.
+//
+// Pass 1 (rows): spec rows -> objcrop rows, direct global loads/stores
+//   (lane t reads x[M t + c + 16 M j]: each (c, j) covers 16*M contiguous
+//   complex per group; it writes X[t + 16 r + 256 p]: 128 contiguous bytes).
+// Pass 2 (columns, in place): a block stages a strip of G columns x L rows
+//   through LDS (rows of G*8 contiguous bytes), each group transforms one
+//   column in registers, scales by 1/L^2 and the strip is written back.
+// HBM: 2 x 2 x 8 L^2 bytes per patch per iteration.
+#include <hip/hip_runtime.h>
+
+#include "dft16.hpp"
+#include "fpm_state.hpp"
+
+namespace fpm {
+
+namespace {
+
+// 256-point DFT of x[m] (m = t + 16 j held as v[j]) -> out[r] = X[t + 16 r]
+template <bool INV>
+__device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], float2 *scr,
+                                            const float2 (&wt)[16], int t, int xrd) {
+    float2 y[16];
+    dft16<INV>(v, y);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], INV ? cconj(wt[k1]) : wt[k1]);
+    float2 z[16];
+    exchange16(scr, t, xrd, y, z);
+    dft16<INV>(z, out);
+}
+
+template <int M, bool INV>
+__device__ __forceinline__ void dftM(float2 *v) {
+    if (M == 2) dft2<INV>(v);
+    if (M == 3) dft3<INV>(v);
+    if (M == 4) dft4<INV>(v);
+}
+
+// x[c][j] = element M*(t + 16 j) + c;  on return x[p][r] = X[t + 16 r + 256 p]
+template <int M, bool INV>
+__device__ __forceinline__ void dftL_regs(float2 (&x)[M][16], float2 *scr, const float2 (&wt)[16],
+                                          const float2 *twL, int t, int xrd) {
+#pragma unroll
+    for (int c = 0; c < M; ++c) {
+        float2 o[16];
+        dft256_full<INV>(x[c], o, scr, wt, t, xrd);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) x[c][r] = o[r];
+    }
+    constexpr int L = 256 * M;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int kp = t + 16 * r;
+        float2 z[M];
+        z[0] = x[0][r];
+#pragma unroll
+        for (int c = 1; c < M; ++c) {
+            const float2 w = twL[(c * kp) % L];
+            z[c] = cmul(x[c][r], INV ? cconj(w) : w);
+        }
+        dftM<M, INV>(z);
+#pragma unroll
+        for (int p = 0; p < M; ++p) x[p][r] = z[p];
+    }
+}
+
+// per-lane four-step twiddles W256^{m t} and the W_L table, staged in LDS
+__device__ __forceinline__ void load_twiddles(float2 *twL, const float2 *__restrict__ tw_L, int L, int step,
+                                              float2 (&wt)[16], int t) {
+    for (int i = threadIdx.x; i < L; i += blockDim.x) twL[i] = tw_L[i];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) wt[m] = twL[((m * t) & 255) * step];  // W256^{mt} = W_L^{M m t}
+}
+
+// pass 1: row IDFTs of fftShift(spec).  grid (L / G, B), block 16 G
+template <int M, int G>
+__global__ void __launch_bounds__(16 * G) k_crop_rows(const float2 *__restrict__ spec, float2 *__restrict__ out,
+                                                      const float2 *__restrict__ tw_L) {
+    constexpr int L = 256 * M;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2 *twL = sm;                  // L
+    float2 *scr_all = sm + L;          // G exchange tiles
+    const int g = threadIdx.x >> 4, t = threadIdx.x & 15;
+    const int xrd = opaque_int(t * XP);
+    float2 *scr = scr_all + g * XTILE;
+    float2 wt[16];
+    load_twiddles(twL, tw_L, L, M, wt, t);
+    const int b = blockIdx.y, row = blockIdx.x * G + g;
+    const int srow = row + L / 2 < L ? row + L / 2 : row - L / 2;       // objF row = spec row + L/2
+    const float2 *src = spec + (size_t)b * L * L + (size_t)srow * L;
+    float2 x[M][16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int c = 0; c < M; ++c) x[c][(j + 8) & 15] = src[M * (t + 16 * j) + c];  // element roll by L/2
+    dftL_regs<M, true>(x, scr, wt, twL, t, xrd);
+    float2 *dst = out + (size_t)b * L * L + (size_t)row * L;
+#pragma unroll
+    for (int p = 0; p < M; ++p)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[t + 16 * r + 256 * p] = x[p][r];
+}
+
+// pass 2: column IDFTs in place, scaled 1/L^2.  grid (L / G, B), block 16 G.
+// The strip goes through LDS in two halves of L/2 rows: element i of a column
+// is in half i / (L/2), i.e. register j / 8 on input (i = M (t + 16 j) + c) and
+// the compile-time set r + 16 p < 8 M on output (k = t + 16 r + 256 p), so a
+// half-size strip (58 KB at L = 768) lets two blocks share a CU and overlap
+// one block's HBM phase with the other's transform.
+template <int M, int G>
+__global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
+                                                      float scale) {
+    constexpr int L = 256 * M, H = L / 2;
+    constexpr int SP = G + 1;          // strip row pitch (complex)
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2 *twL = sm;                  // L
+    float2 *strip = sm + L;            // H x SP
+    float2 *scr_all = strip;           // G exchange tiles, inside the strip: used
+                                       // only while every column is in registers
+    const int g = threadIdx.x >> 4, t = threadIdx.x & 15;
+    const int xrd = opaque_int(t * XP);
+    float2 *scr = scr_all + g * XTILE;
+    float2 wt[16];
+    load_twiddles(twL, tw_L, L, M, wt, t);
+    const int b = blockIdx.y, c0 = blockIdx.x * G;
+    float2 *base = io + (size_t)b * L * L + c0;
+    constexpr int NTH = 16 * G;
+    float2 x[M][16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        // strip load: consecutive threads take consecutive columns of a row
+#pragma unroll 4
+        for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
+            const int y = idx / G, cc = idx - y * G;
+            strip[y * SP + cc] = base[(size_t)(y + h * H) * L + cc];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 8 * h; j < 8 * h + 8; ++j)
+#pragma unroll
+            for (int c = 0; c < M; ++c) x[c][j] = strip[(M * (t + 16 * j) + c - h * H) * SP + g];
+        __syncthreads();
+    }
+    dftL_regs<M, true>(x, scr, wt, twL, t, xrd);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        __syncthreads();  // exchange tiles / previous half's reads are done
+#pragma unroll
+        for (int p = 0; p < M; ++p)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if ((r + 16 * p < 8 * M) == (h == 0))
+                    strip[(t + 16 * r + 256 * p - h * H) * SP + g] = cscale(x[p][r], scale);
+        __syncthreads();
+#pragma unroll 4
+        for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
+            const int y = idx / G, cc = idx - y * G;
+            base[(size_t)(y + h * H) * L + cc] = strip[y * SP + cc];
+        }
+    }
+}
+
+template <int M, int GR, int G>
+hipError_t launch_crop(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
+    constexpr int L = 256 * M;
+    const size_t lds_rows = (size_t)(L + GR * XTILE) * sizeof(float2);
+    static_assert(G * XTILE <= L / 2 * (G + 1), "exchange tiles must fit in the half strip");
+    const size_t lds_cols = (size_t)(L + L / 2 * (G + 1)) * sizeof(float2);
+    hipError_t e = hipFuncSetAttribute((const void *)k_crop_rows<M, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds_rows);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_crop_cols<M, G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_cols);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_crop_rows<M, GR>), dim3(L / GR, st.B), dim3(16 * GR), lds_rows, s,
+                       (const float2 *)st.spec, out, tw_L);
+    hipLaunchKernelGGL((k_crop_cols<M, G>), dim3(L / G, st.B), dim3(16 * G), lds_cols, s, out, tw_L,
+                       1.0f / ((float)L * (float)L));
+    return hipGetLastError();
+}
+
+}  // namespace
+
+#ifndef FPM_CROP_G
+#define FPM_CROP_G 16   // columns per strip: 128-byte row segments
+#endif
+#ifndef FPM_CROP_GR
+#define FPM_CROP_GR 4   // rows per block in the row pass
+#endif
+
+// hipErrorNotSupported when L is not 512 / 768 / 1024 (caller falls back to
+// the mixed-radix batched transform)
+hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
+    switch (st.L) {
+        case 512: return launch_crop<2, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
+        case 768: return launch_crop<3, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
+        case 1024: return launch_crop<4, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+}  // namespace fpm
