@@ -388,8 +388,8 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipMemset(c->dbg, 0, sizeof h));
         const double steps = (double)iters * c->prob.n_order * c->st.B;
         fprintf(stderr, "[fpm stamps] cycles per LED step (wave 0 view, mean over blocks):");
-        const char *names[7] = {"A:rowIDFT", "A:tail", "B:columns", "C:rowDFT+upd", "C:tail", "D:tiles", "D:max+P"};
-        for (int i = 0; i < 7; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / steps);
+        const char *names[8] = {"gather", "A:tail+sync", "B:columns", "C:rowDFT", "update", "max", "P", "A:rowIDFT"};
+        for (int i = 0; i < 8; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / steps);
         fprintf(stderr, "\n");
     }
     c->timing.led_launch_ms = c->timing.led_launches ? led_ms / c->timing.led_launches : 0.0;

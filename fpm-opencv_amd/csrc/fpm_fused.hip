@@ -63,7 +63,9 @@ struct FusedArgs {
     int n_tail_rows;
     int tail_ky[fz::MAXTAILROWS];  // sigma = 64 + i
     int n_tail_px;
-    int2 tail_px[fz::MAXTAIL];  // (ky, kx)
+    int2 tail_px[fz::MAXTAIL];  // (ky, kx), sorted by row then kx
+    // tail row q holds pixels tail_px[p0 .. p0+np) with kx = kx0, kx0+1, ...
+    int tail_row_p0[fz::MAXTAILROWS], tail_row_np[fz::MAXTAILROWS], tail_row_kx0[fz::MAXTAILROWS];
     int ntiles, nwords;         // tiles of |spec| maxima, 32-bit words of the dirty bitmap
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
 };
@@ -290,7 +292,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     __syncthreads();
 
     // diagnostic: shader-clock cycles per phase, summed over LEDs (wave-uniform)
-    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // phases: see api.cpp stamp names
     unsigned long long prev = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
 #define FPM_STAMP(i)                                                  \
     if (a.dbg) {                                                      \
@@ -376,15 +378,24 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                     for (int m = 0; m < 8; ++m) row[16 * m] = r[8 + m];
                 }
             }
+            FPM_STAMP(7)
             for (int idx = tid; idx < a.n_tail_rows * TH; idx += NT) {  // tail rows: direct sums
+                // q is wave-uniform (TH = 2 waves): the row's pixel range comes
+                // from scalar loads; kx runs over a contiguous range, so the
+                // twiddle index advances by x per term
                 const int q = idx / TH, xl = idx - q * TH, x = xl + TH * h;
-                const int rky = tky[q];
-                float2 s2 = make_float2(0.f, 0.f);
-                for (int p = 0; p < a.n_tail_px; ++p) {
-                    if (tpx[p].x != rky) continue;
-                    s2 = cadd(s2, cmul(tailX[p], cconj(tw[(x * (tpx[p].y + NP)) & (NP - 1)])));
+                const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
+                int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
+                float2 s2 = make_float2(0.f, 0.f), s3 = make_float2(0.f, 0.f);
+                int p = 0;
+                for (; p + 1 < np_; p += 2) {
+                    const int tj = (ti + x) & (NP - 1);
+                    s2 = cadd(s2, cmul(tailX[p0 + p], cconj(tw[ti])));
+                    s3 = cadd(s3, cmul(tailX[p0 + p + 1], cconj(tw[tj])));
+                    ti = (tj + x) & (NP - 1);
                 }
-                th[(NROWS + q) * TLD + xl] = s2;
+                if (p < np_) s2 = cadd(s2, cmul(tailX[p0 + p], cconj(tw[ti])));
+                th[(NROWS + q) * TLD + xl] = cadd(s2, s3);
             }
             __syncthreads();  // half-T complete
             FPM_STAMP(1)
@@ -615,7 +626,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     }
 #undef FPM_STAMP
     if (a.dbg && tid == 0)
-        for (int i = 0; i < 7; ++i) atomicAdd(&a.dbg[i], acc[i]);
+        for (int i = 0; i < 8; ++i) atomicAdd(&a.dbg[i], acc[i]);
 
     // ---- write back the per-patch state
 #pragma unroll
@@ -734,6 +745,17 @@ hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, co
     a.n_tail_rows = g.n_tail_rows;
     for (int i = 0; i < fz::MAXTAILROWS; ++i) a.tail_ky[i] = g.tail_ky[i];
     a.n_tail_px = g.n_tail_px;
+    for (int q = 0; q < fz::MAXTAILROWS; ++q) {
+        a.tail_row_p0[q] = a.tail_row_np[q] = a.tail_row_kx0[q] = 0;
+        for (int p = 0; p < g.n_tail_px && q < g.n_tail_rows; ++p)
+            if (g.tail_px[p].x == g.tail_ky[q]) {
+                if (a.tail_row_np[q] == 0) {
+                    a.tail_row_p0[q] = p;
+                    a.tail_row_kx0[q] = g.tail_px[p].y;
+                }
+                ++a.tail_row_np[q];
+            }
+    }
     for (int i = 0; i < fz::MAXTAIL; ++i) a.tail_px[i] = i < g.n_tail_px ? g.tail_px[i] : make_int2(0, 0);
     a.ntiles = st.ntx * st.nty;
     a.nwords = (a.ntiles + 31) / 32;
