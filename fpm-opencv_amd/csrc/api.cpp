@@ -38,6 +38,10 @@ hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, co
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   unsigned long long *dbg, hipStream_t s);
 size_t fused_meas_bytes(int np, int B, int n_stack);
+hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
+                                   const int *py0_dev, int bk1x, int bk1y, int bk2x, int bk2y, double bg_threshold,
+                                   double dark_mult, bool darkfield, unsigned long long *sums, uint16_t *out,
+                                   int16_t *bg_out_dev, hipStream_t s);
 size_t fused_T_elems(int np, int r, int B);
 }  // namespace fpm
 
@@ -169,6 +173,25 @@ int validate(const fpm_problem *p) {
 }
 
 }  // namespace
+
+namespace {
+// device scratch owned by one fpm_upload_frames call
+struct Scratch {
+    std::vector<void *> p;
+    ~Scratch() {
+        for (void *q : p) (void)hipFree(q);
+    }
+    template <typename T>
+    hipError_t get(T **out, size_t n) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, n * sizeof(T) > 0 ? n * sizeof(T) : 16);
+        if (e == hipSuccess) p.push_back(q);
+        *out = (T *)q;
+        return e;
+    }
+};
+}  // namespace
+
 
 extern "C" {
 
@@ -319,6 +342,58 @@ int fpm_upload_stack_device(fpm_ctx *c, const uint16_t *meas) {
     const size_t n = (size_t)c->prob.n_stack * c->st.B * c->st.np * c->st.np;
     HIP_TRY(hipMemcpyAsync(c->meas, meas, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, c->stream));
     return after_upload(c);
+}
+
+int fpm_upload_frames(fpm_ctx *c, const fpm_frames *f, const uint16_t *data, int on_device, int16_t *bg_val) {
+    if (!c || !f || !data || !f->patch_x0 || !f->patch_y0) return set_err(FPM_ERR_INVAL, "null argument");
+    const int np = c->st.np, B = c->st.B, H = f->height, W = f->width, n = c->prob.n_stack;
+    if (H < np || W < np) return set_err(FPM_ERR_INVAL, "frame %dx%d smaller than Np=%d", H, W, np);
+    auto inside = [&](int x, int y) { return x >= 0 && y >= 0 && x + np <= W && y + np <= H; };
+    for (int b = 0; b < B; ++b)
+        if (!inside(f->patch_x0[b], f->patch_y0[b]))
+            return set_err(FPM_ERR_INVAL, "patch %d window (%d,%d) outside the %dx%d frame", b, f->patch_x0[b],
+                           f->patch_y0[b], W, H);
+    if (!inside(f->bk1_x, f->bk1_y) || !inside(f->bk2_x, f->bk2_y))
+        return set_err(FPM_ERR_INVAL, "background window outside the frame (cv::Rect assertion in the reference)");
+    if (!(f->darkfield_exp_multiplier > 0.0)) return set_err(FPM_ERR_INVAL, "darkfieldExpMultiplier must be > 0");
+    HIP_TRY(hipSetDevice(c->device));
+    Scratch sc;
+    int *px0 = nullptr, *py0 = nullptr;
+    unsigned long long *sums = nullptr;
+    int16_t *bg_dev = nullptr;
+    uint16_t *stage = nullptr;
+    HIP_TRY(sc.get(&px0, B));
+    HIP_TRY(sc.get(&py0, B));
+    HIP_TRY(sc.get(&sums, 2 * (size_t)n));
+    HIP_TRY(sc.get(&bg_dev, n));
+    HIP_TRY(hipMemcpyAsync(px0, f->patch_x0, B * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(py0, f->patch_y0, B * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    const size_t fpx = (size_t)H * W;
+    if (!on_device) HIP_TRY(sc.get(&stage, fpx));
+    for (int i = 0; i < n; ++i) {
+        const uint16_t *frame = data + (size_t)i * fpx;
+        if (!on_device) {  // host frames go through one staging buffer (PCIe)
+            HIP_TRY(hipMemcpyAsync(stage, frame, fpx * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+            frame = stage;
+        }
+        HIP_TRY(launch_preprocess_frame(frame, W, np, B, px0, py0, f->bk1_x, f->bk1_y, f->bk2_x, f->bk2_y,
+                                        f->bg_threshold, f->darkfield_exp_multiplier,
+                                        f->darkfield ? f->darkfield[i] != 0 : false, sums + 2 * i,
+                                        c->meas + (size_t)i * B * np * np, bg_dev + i, c->stream));
+    }
+    if (bg_val) HIP_TRY(hipMemcpyAsync(bg_val, bg_dev, n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // scratch is freed on return
+    return after_upload(c);
+}
+
+int fpm_download_stack(fpm_ctx *c, uint16_t *meas) {
+    if (!c || !meas) return set_err(FPM_ERR_INVAL, "null argument");
+    if (!c->uploaded) return set_err(FPM_ERR_STATE, "no stack uploaded");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = (size_t)c->prob.n_stack * c->st.B * c->st.np * c->st.np;
+    HIP_TRY(hipMemcpyAsync(meas, c->meas, n * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return FPM_OK;
 }
 
 int fpm_init(fpm_ctx *c) {

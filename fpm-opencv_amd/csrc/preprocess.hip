@@ -1,0 +1,82 @@
+// preprocess.hip -- loadFPMDataset's per-image preprocessing on the device
+// (fpmMain.cpp:124-144), for n_patch patches cut from every full frame.
+//
+// Per frame (one LED image):
+//   k_bg_sums      exact uint64 sums of the two Np x Np background windows of
+//                  the undivided frame (cv::mean accumulates in double, which
+//                  is exact for these integer sums; so is uint64)
+//   k_crop_patches bg = clamp((mean1 + mean2)/2, bgThresh) rounded to int16,
+//                  then for each patch pixel: crop, optional darkfield divide
+//                  (saturate_cast<ushort>(rint(v / m)), round half to even),
+//                  saturating subtract of bg -> meas[led][patch][y][x]
+// HBM-bound byte work: 2 B read + 2 B written per patch pixel plus 2 x 2 Np^2 B
+// of background windows per frame.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fpm {
+
+namespace {
+
+// sums[w] += window w pixels.  grid (np, 2), block 256: one window row per block
+__global__ void __launch_bounds__(256) k_bg_sums(const uint16_t *__restrict__ frame, int width, int np, int bk1x,
+                                                 int bk1y, int bk2x, int bk2y, unsigned long long *sums) {
+    __shared__ unsigned long long part[4];
+    const int w = blockIdx.y, y = blockIdx.x;
+    const int x0 = w ? bk2x : bk1x, y0 = w ? bk2y : bk1y;
+    const uint16_t *row = frame + (size_t)(y0 + y) * width + x0;
+    unsigned long long s = 0;
+    for (int x = threadIdx.x; x < np; x += 256) s += row[x];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&sums[w], part[0] + part[1] + part[2] + part[3]);
+}
+
+__device__ __forceinline__ int bg_value(const unsigned long long *sums, int np, double bg_threshold) {
+    const double n2 = (double)np * (double)np;
+    double bg = ((double)sums[1] / n2 + (double)sums[0] / n2) / 2;  // (bk2 + bk1) / 2, fpmMain.cpp:136
+    if (bg > bg_threshold) bg = bg_threshold;                       // :137-138
+    return (int)(int16_t)round(bg);                                 // :140
+}
+
+// grid (np, B), block 256: row y of patch b
+__global__ void __launch_bounds__(256) k_crop_patches(const uint16_t *__restrict__ frame, int width, int np,
+                                                      const int *__restrict__ px0, const int *__restrict__ py0,
+                                                      const unsigned long long *__restrict__ sums,
+                                                      double bg_threshold, double dark_mult, int darkfield,
+                                                      uint16_t *__restrict__ out, int16_t *bg_out) {
+    const int y = blockIdx.x, b = blockIdx.y;
+    const int bg = bg_value(sums, np, bg_threshold);
+    if (y == 0 && b == 0 && threadIdx.x == 0 && bg_out) *bg_out = (int16_t)bg;
+    const uint16_t *src = frame + (size_t)(py0[b] + y) * width + px0[b];
+    uint16_t *dst = out + ((size_t)b * np + y) * np;
+    for (int x = threadIdx.x; x < np; x += 256) {
+        int v = src[x];
+        if (darkfield) {  // :128-129, saturate_cast rounds to nearest even
+            const double q = rint((double)v / dark_mult);
+            v = q < 0.0 ? 0 : (q > 65535.0 ? 65535 : (int)q);
+        }
+        v -= bg;  // :143-144 saturating
+        dst[x] = (uint16_t)(v < 0 ? 0 : (v > 65535 ? 65535 : v));
+    }
+}
+
+}  // namespace
+
+// One frame -> meas slab [B][np][np].  `sums` is 2 device uint64 (zeroed here).
+hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
+                                   const int *py0_dev, int bk1x, int bk1y, int bk2x, int bk2y, double bg_threshold,
+                                   double dark_mult, bool darkfield, unsigned long long *sums, uint16_t *out,
+                                   int16_t *bg_out_dev, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bg_sums, dim3(np, 2), dim3(256), 0, s, frame, width, np, bk1x, bk1y, bk2x, bk2y, sums);
+    hipLaunchKernelGGL(k_crop_patches, dim3(np, B), dim3(256), 0, s, frame, width, np, px0_dev, py0_dev,
+                       (const unsigned long long *)sums, bg_threshold, dark_mult,
+                       (darkfield && dark_mult != 1.0) ? 1 : 0, out, bg_out_dev);
+    return hipGetLastError();
+}
+
+}  // namespace fpm

@@ -8,7 +8,8 @@
 // sec)").  The solver runs on the MI355X through libfpm_hip.so.  Instead of
 // the reference's blocking showComplexImg windows (fpmMain.cpp:495-497) the
 // results are written as .npy files: objCrop (L x L complex64), objF
-// (un-centred spectrum), pupil (centred, Np x Np complex64).
+// (un-centred spectrum), pupil (centred, Np x Np complex64), plus a
+// result.json sidecar (geometry, LED order, iterations, timing).
 //
 // Extra options (after the two positional arguments):
 //   --out DIR          output directory (default ".")
@@ -183,11 +184,31 @@ int main(int argc, char **argv) {
         std::cerr << "fpm: " << fpm_last_error() << std::endl;
         return 1;
     }
+    fpm_info info;
+    fpm_get_info(ctx, &info);
     fpm_destroy(ctx);
     fpm_host_close(h);
     bool ok = write_npy_c64(out_dir + "/objCrop.npy", objCrop.data(), L, L) &&
               write_npy_c64(out_dir + "/objF.npy", objF.data(), L, L) &&
               write_npy_c64(out_dir + "/pupil.npy", pupil.data(), np, np);
+    if (ok) {  // JSON sidecar describing the arrays (replaces the reference's display windows)
+        FILE *f = fopen((out_dir + "/result.json").c_str(), "w");
+        ok = f != nullptr;
+        if (f) {
+            fprintf(f, "{\n  \"dataset\": \"%s\",\n  \"iterations\": %d,\n  \"np\": %d,\n  \"nlarge\": %d,\n",
+                    argv[1], itr_count, np, L);
+            fprintf(f, "  \"na_radius\": %d,\n  \"delta1\": %g,\n  \"delta2\": %g,\n  \"leds_used\": %d,\n",
+                    cfg.na_radius, cfg.delta1, cfg.delta2, used);
+            fprintf(f, "  \"path\": \"%s\",\n  \"seconds\": %.6f,\n  \"order\": [",
+                    info.path == FPM_PATH_FUSED ? "fused" : "general", dt);
+            for (int i = 0; i < used; ++i) fprintf(f, "%s%d", i ? ", " : "", order[i]);
+            fprintf(f, "],\n  \"arrays\": {\n");
+            fprintf(f, "    \"objCrop.npy\": \"complex64 [Nlarge][Nlarge], IDFT(objF)/Nlarge^2 (fpmMain.cpp:481)\",\n");
+            fprintf(f, "    \"objF.npy\": \"complex64 [Nlarge][Nlarge], un-centred object spectrum\",\n");
+            fprintf(f, "    \"pupil.npy\": \"complex64 [Np][Np], centred pupil (fpmMain.cpp:496)\"\n  }\n}\n");
+            fclose(f);
+        }
+    }
     if (!ok) {
         std::cerr << "cannot write outputs to " << out_dir << std::endl;
         return 1;

@@ -37,6 +37,7 @@ HIP_SYMBOLS = (
     "fpm_init", "fpm_run", "fpm_synchronize", "fpm_download",
     "fpm_download_objcrop_device", "fpm_set_stream", "fpm_get_info",
     "fpm_get_timing", "fpm_runFPM", "fpm_last_error", "fpm_version",
+    "fpm_upload_frames", "fpm_download_stack",
 )
 
 
@@ -54,6 +55,16 @@ class fpm_problem(C.Structure):
         ("na_radius", C.c_int32), ("init_pos", C.c_int32),
         ("delta1", C.c_double), ("delta2", C.c_double), ("eps", C.c_double),
         ("n_patch", C.c_int32), ("path", C.c_int32), ("flags", C.c_uint32),
+    ]
+
+
+class fpm_frames(C.Structure):
+    _fields_ = [
+        ("height", C.c_int32), ("width", C.c_int32),
+        ("patch_x0", C.POINTER(C.c_int32)), ("patch_y0", C.POINTER(C.c_int32)),
+        ("bk1_x", C.c_int32), ("bk1_y", C.c_int32), ("bk2_x", C.c_int32), ("bk2_y", C.c_int32),
+        ("bg_threshold", C.c_double), ("darkfield_exp_multiplier", C.c_double),
+        ("darkfield", C.POINTER(C.c_uint8)),
     ]
 
 
@@ -98,6 +109,8 @@ def load_library(path: str = HIP_LIB):
         "fpm_get_timing": (C.c_int, [vp, C.POINTER(fpm_timing)]),
         "fpm_runFPM": (C.c_int, [C.POINTER(fpm_problem), C.c_int, u16p, C.c_int,
                                  f32p, f32p, f32p, f32p]),
+        "fpm_upload_frames": (C.c_int, [vp, C.POINTER(fpm_frames), vp, C.c_int, C.POINTER(C.c_int16)]),
+        "fpm_download_stack": (C.c_int, [vp, u16p]),
         "fpm_last_error": (C.c_char_p, []),
         "fpm_version": (C.c_char_p, []),
     }
@@ -196,6 +209,41 @@ class Solver:
         if a.shape != want:
             raise ValueError(f"stack shape {a.shape} != {want}")
         _check(_lib.fpm_upload_stack(self._h, a.ctypes.data_as(C.POINTER(C.c_uint16))))
+
+    def upload_frames(self, frames, patch_x0, patch_y0, bk1=(1, 1), bk2=(1, 1), bg_threshold=1000.0,
+                      darkfield_exp_multiplier=1.0, darkfield=None, device_ptr: int | None = None,
+                      shape=None):
+        """Loader preprocessing on the GPU (fpmMain.cpp:124-144): `frames` is
+        uint16 [n_stack][H][W] on the host, or pass device_ptr (+ shape=(H, W))
+        for frames already in device memory.  Returns the int16 bg_val per image."""
+        p = self.prob
+        n = len(p.x0)
+        if device_ptr is None:
+            a = np.ascontiguousarray(frames, dtype=np.uint16)
+            if a.ndim != 3 or a.shape[0] != n:
+                raise ValueError(f"frames shape {a.shape}: want [{n}][H][W]")
+            H, W = a.shape[1:]
+            data = a.ctypes.data_as(C.c_void_p)
+        else:
+            H, W = shape
+            data = C.c_void_p(device_ptr)
+        px, py = _i32(patch_x0), _i32(patch_y0)
+        if len(px) != p.n_patch or len(py) != p.n_patch:
+            raise ValueError("one (x0, y0) per patch")
+        dark = np.ascontiguousarray(np.zeros(n, np.uint8) if darkfield is None else np.asarray(darkfield, np.uint8))
+        f = fpm_frames(int(H), int(W), px.ctypes.data_as(C.POINTER(C.c_int32)), py.ctypes.data_as(C.POINTER(C.c_int32)),
+                       int(bk1[0]), int(bk1[1]), int(bk2[0]), int(bk2[1]), float(bg_threshold),
+                       float(darkfield_exp_multiplier), dark.ctypes.data_as(C.POINTER(C.c_uint8)))
+        bg = np.zeros(n, np.int16)
+        _check(_lib.fpm_upload_frames(self._h, C.byref(f), data, 0 if device_ptr is None else 1,
+                                      bg.ctypes.data_as(C.POINTER(C.c_int16))))
+        return bg
+
+    def download_stack(self) -> np.ndarray:
+        p = self.prob
+        out = np.empty((len(p.x0), p.n_patch, p.np_, p.np_), np.uint16)
+        _check(_lib.fpm_download_stack(self._h, out.ctypes.data_as(C.POINTER(C.c_uint16))))
+        return out
 
     def upload_device(self, ptr: int):
         _check(_lib.fpm_upload_stack_device(self._h, C.c_void_p(ptr)))

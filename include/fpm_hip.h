@@ -41,6 +41,29 @@ extern "C" {
 #define FPM_PATH_GENERAL  1     /* 4 kernels per LED step, any Np / radius   */
 #define FPM_PATH_FUSED    2     /* one persistent launch per iteration       */
 
+/*
+ * Raw sensor frames for fpm_upload_frames: the loader preprocessing of
+ * loadFPMDataset (fpmMain.cpp:124-144) on the device, for n_patch patches
+ * cut from each full frame:
+ *   Image  = frame[patch_y0 + y][patch_x0 + x]                 (:124-125)
+ *   Image  = saturate(rint(Image / darkfield_exp_multiplier))  when darkfield[i]
+ *            and the multiplier != 1                            (:128-129)
+ *   bg     = (mean(bk1 window) + mean(bk2 window)) / 2 of the UNDIVIDED
+ *            frame, clamped to bg_threshold, rounded to int16   (:131-140)
+ *   Image  = saturate(Image - bg)                               (:143-144)
+ * Background windows are Np x Np and shared by all patches of a frame.
+ */
+typedef struct fpm_frames {
+    int32_t height, width;        /* full frame size                              */
+    const int32_t *patch_x0;      /* [n_patch] cropX of each patch (column)       */
+    const int32_t *patch_y0;      /* [n_patch] cropY of each patch (row)          */
+    int32_t bk1_x, bk1_y;         /* bk1cropX / bk1cropY                          */
+    int32_t bk2_x, bk2_y;         /* bk2cropX / bk2cropY                          */
+    double  bg_threshold;         /* bgThresh (JSON asInt)                        */
+    double  darkfield_exp_multiplier;  /* darkfieldExpMultiplier                  */
+    const uint8_t *darkfield;     /* [n_stack] 1 where illumination NA > objective NA */
+} fpm_frames;
+
 /* fpm_problem.flags */
 #define FPM_FLAG_OBJCROP_LAST_ONLY 1u  /* compute objCrop only after the last
                                           iteration of fpm_run (the reference
@@ -101,6 +124,16 @@ void fpm_destroy(fpm_ctx *ctx);
 int  fpm_upload_stack(fpm_ctx *ctx, const uint16_t *meas);
 /* Same, from device memory on the context's device (no PCIe round trip). */
 int  fpm_upload_stack_device(fpm_ctx *ctx, const uint16_t *meas_dev);
+
+/* Upload raw frames [n_stack][height][width] (host memory, or device memory on
+ * the context's device when frames_on_device != 0) and build the measurement
+ * stack on the GPU (fpm_frames above).  bg_val, when not NULL, receives the
+ * per-image background [n_stack] (FPMImage::bg_val, fpmMain.h:33). */
+int  fpm_upload_frames(fpm_ctx *ctx, const fpm_frames *frames, const uint16_t *data,
+                       int frames_on_device, int16_t *bg_val);
+
+/* Copy the measurement stack [n_stack][n_patch][Np][Np] back to the host. */
+int  fpm_download_stack(fpm_ctx *ctx, uint16_t *meas);
 
 /* fpmMain.cpp:302-343: pupil = support disk, spectrum from order[init_pos]. */
 int  fpm_init(fpm_ctx *ctx);

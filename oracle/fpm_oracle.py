@@ -14,6 +14,7 @@ side by side with the reference:
 * per-LED update .................. fpmMain.cpp:348-476
 * per-iteration objCrop IDFT ...... fpmMain.cpp:481
 * pupil re-centred at exit ........ fpmMain.cpp:496
+* loader preprocessing ............ fpmMain.cpp:124-144 (``preprocess_frame``)
 
 Semantics of the un-vendored ``cvComplex`` helpers are *assumed* as listed in
 SURVEY.md section 8(c) (i)-(vii): ``fft2`` = unscaled forward DFT, ``ifft2`` =
@@ -151,3 +152,34 @@ def rel_l2(a, b) -> float:
     b = np.asarray(b, np.complex128)
     den = np.linalg.norm(b.ravel())
     return float(np.linalg.norm((a - b).ravel()) / (den if den > 0 else 1.0))
+
+
+def preprocess_frame(frame, np_: int, crop, bk1, bk2, bg_threshold: float, dark_mult: float = 1.0,
+                     darkfield: bool = False):
+    """loadFPMDataset's per-image preprocessing (fpmMain.cpp:124-144) for one
+    patch window ``crop`` = (x, y) of a full uint16 frame [H][W]:
+
+    * crop ``Image = fullImg(Rect(cropX, cropY, Np, Np))``           (:124-125)
+    * darkfield ``cv::divide(Image, mult)`` when the LED NA > objective NA and
+      mult != 1: saturate_cast<ushort> of the quotient, round half to even (:128-129)
+    * ``bg = (mean(bk2 window) + mean(bk1 window)) / 2`` of the UNDIVIDED frame,
+      clamped to bgThresh, ``(int16_t)round(bg)``                    (:131-140)
+    * saturating ``cv::subtract(Image, bg)``                         (:143-144)
+
+    Returns (uint16 [Np][Np], bg_val)."""
+    f = np.asarray(frame)
+    x, y = crop
+    img = f[y:y + np_, x:x + np_].astype(np.int64)
+    if darkfield and dark_mult != 1:
+        img = np.clip(np.rint(img / float(dark_mult)), 0, 65535).astype(np.int64)
+
+    def mean(w):
+        wx, wy = w
+        return float(f[wy:wy + np_, wx:wx + np_].astype(np.int64).sum()) / (np_ * np_)
+
+    bg = (mean(bk2) + mean(bk1)) / 2
+    if bg > bg_threshold:
+        bg = float(bg_threshold)
+    bg_val = int(np.floor(bg + 0.5))                       # std::round, bg >= 0
+    bg_val = (bg_val + 32768) % 65536 - 32768               # (int16_t) conversion
+    return np.clip(img - bg_val, 0, 65535).astype(np.uint16), bg_val
