@@ -20,7 +20,8 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("k_fused_iteration", "k_permute_meas", "k_fft_batch<true>", "k_fft_batch<false>"):
+    for k in ("k_fused_iteration", "k_permute_meas", "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows",
+              "k_crop_cols"):
         if k in name:
             return k
     return name[:60]
