@@ -222,6 +222,9 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
     const int xrd = opaque_int(t * XP);  // exchange read base, see exchange16
     const int lane = tid & 63, w = tid >> 6;
+#ifdef FPM_EXP_PRIO
+    if (w >= NT / 128) __builtin_amdgcn_s_setprio(1);  // second-dispatched half wins arbitration
+#endif
     const int b = blockIdx.x;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * XTILE;
@@ -613,15 +616,17 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             Pt = make_float2(Pt.x + NPt.x * rom, Pt.y + NPt.y * rom);
             pmx = fmaxf(pmx, cabs2(Pt));
         }
+        // red[8..15] is not used by the max phase, so no barrier is needed
+        // before writing it; nothing read below is rewritten by another
+        // thread before the next LED's first barrier (numerators sit in this
+        // thread's own half-T slots, tailX was last read in pass A)
         pmx = wave_max(pmx);
-        __syncthreads();  // everyone has read red[] (omax)
-        if (lane == 0) red[w] = pmx;
+        if (lane == 0) red[8 + w] = pmx;
         __syncthreads();
-        float pm2 = red[0];
+        float pm2 = red[8];
 #pragma unroll
-        for (int i = 1; i < NT / 64; ++i) pm2 = fmaxf(pm2, red[i]);
+        for (int i = 1; i < NT / 64; ++i) pm2 = fmaxf(pm2, red[8 + i]);
         pm = sqrtf(pm2);
-        __syncthreads();  // red[], tailX and half-T are reused next LED
         FPM_STAMP(6)
     }
 #undef FPM_STAMP

@@ -28,7 +28,25 @@ CASES = [
     ("dogStomach_metric", "dataset_dogStomach.json", 293, 0.6, 256),
     ("cellScope_literal", "dataset_cellScope.json", 508, None, None),
     ("mono_no_coordinates", "dataset_mono.json", 508, None, None),
+    # SURVEY.md 8(c) fallback: dataset_mono.json optics with the 508-LED dome
+    # table of include/domeHoleCoordinates.h inserted as holeCoordinates
+    ("mono_dome", "dataset_mono.json+dome", 508, None, None),
 ]
+DOME_H = "include/domeHoleCoordinates.h"
+
+
+def dome_table():
+    """The 508 (x, y, z) triples of domeHoleCoordinates.h, read as numbers."""
+    text = open(os.path.join(REF, DOME_H)).read()
+    rows = re.findall(r"\{\s*(-?[0-9.eE+-]+)\s*,\s*(-?[0-9.eE+-]+)\s*,\s*(-?[0-9.eE+-]+)\s*\}", text)
+    assert len(rows) == 508, len(rows)
+    return [[float(a), float(b), float(c)] for a, b, c in rows]
+
+
+def with_dome(text):
+    rows = ",\n".join('   [{"x":%r},{"y":%r},{"z":%r}]' % tuple(r) for r in dome_table())
+    body = text.rstrip().rstrip("}").rstrip().rstrip(",")
+    return body + ',\n  "holeCoordinates":[\n' + rows + "\n]\n}\n"
 
 SCALAR_KEYS = ["cropSizeX", "pixelSize", "objectiveMag", "objectiveNA", "maxIlluminationNA", "lambda",
                "arrayRotation", "bgThresh", "delta1", "delta2", "ledCount", "flipDatasetX", "flipDatasetY",
@@ -49,8 +67,14 @@ def main():
     if not os.path.exists(PROBE):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])
     for name, fn, n, maxna, np_ in CASES:
-        path = os.path.join(REF, fn)
-        text = open(path).read()
+        if fn.endswith("+dome"):
+            text = with_dome(open(os.path.join(REF, fn[:-5])).read())
+            path = "/tmp/fpm_mono_dome.json"
+            with open(path, "w") as f:
+                f.write(text)
+        else:
+            path = os.path.join(REF, fn)
+            text = open(path).read()
         args = [PROBE, path, str(n)]
         if maxna is not None or np_ is not None:
             args += [str(maxna if maxna is not None else 0.7604 if "maxIlluminationNA" not in text else
@@ -58,7 +82,7 @@ def main():
         if np_ is not None:
             args += [str(np_)]
         probe = json.loads(subprocess.check_output(args).decode())
-        fixture = dict(source=fn, n_present=n, max_na_override=maxna, np_override=np_,
+        fixture = dict(source=fn if not fn.endswith("+dome") else fn[:-5] + " + " + DOME_H, n_present=n, max_na_override=maxna, np_override=np_,
                        keys=scalar_keys(text),
                        trailing_comma=bool(re.search(r",\s*\]\s*\}\s*$", text)),
                        probe=probe)

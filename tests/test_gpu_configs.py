@@ -1,0 +1,63 @@
+"""BASELINE.json configs 1-2 as parity cases (GPU only): dataset_mono optics
+with the 508-LED dome table (SURVEY.md 8(c) fallback; geometry and LED order
+from the reference's own jsoncpp probe, tests/golden/geometry_mono_dome.json):
+Np 90, L 360, naRadius 30, 193 LEDs -- the general (mixed radix 2/3/5) path.
+
+  config 1: 1 patch, 5 iterations, vs the C++ fp64 oracle
+  config 2: 64 patches batched on one GPU; sampled patches vs the oracle
+Tolerance: relative L2 <= 1e-4 after 5 iterations (SURVEY.md 8(c) proposes
+1e-3), <= 1e-5 after 1 iteration.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import fpm_amd
+from fpm_oracle import rel_l2
+from tools.synth import make_stack
+
+pytestmark = pytest.mark.gpu
+
+FIX = os.path.join(os.path.dirname(__file__), "golden", "geometry_mono_dome.json")
+
+
+def _geometry():
+    p = json.load(open(FIX))["probe"]
+    leds = {l["led"]: l for l in p["leds"]}
+    order = p["sorted_indices"]
+    x0 = np.array([leds[n]["crop_x0"] for n in order], np.int32)
+    y0 = np.array([leds[n]["crop_y0"] for n in order], np.int32)
+    return p, x0, y0
+
+
+def test_config1_mono_dome_single_patch_5_iterations():
+    import oracle_lib
+    p, x0, y0 = _geometry()
+    Np, L, r = p["np"], p["nlarge"], p["na_radius"]
+    assert (Np, L, r, len(x0)) == (90, 360, 30, 193)
+    order = np.arange(len(x0))
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=11)
+    ref = oracle_lib.run_fpm(stack[:, 0], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 5)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=1)
+    out = fpm_amd.run_fpm(prob, stack, 5)
+    for k in ("objCrop", "objF", "pupil"):
+        e = rel_l2(out[k][0], ref[k])
+        assert e < 1e-4, (k, e)
+
+
+def test_config2_mono_dome_64_patches_batched():
+    import oracle_lib
+    p, x0, y0 = _geometry()
+    Np, L, r = p["np"], p["nlarge"], p["na_radius"]
+    order = np.arange(len(x0))
+    B = 64
+    stack = make_stack(Np, L, r, x0, y0, n_patch=B, seed=12)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=B)
+    out = fpm_amd.run_fpm(prob, stack, 1)
+    assert np.isfinite(out["objCrop"]).all()
+    for b in (0, 37, 63):
+        ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 1)
+        assert rel_l2(out["objCrop"][b], ref["objCrop"]) < 1e-5
+        assert rel_l2(out["pupil"][b], ref["pupil"]) < 1e-5
