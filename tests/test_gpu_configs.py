@@ -61,3 +61,23 @@ def test_config2_mono_dome_64_patches_batched():
         ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 1)
         assert rel_l2(out["objCrop"][b], ref["objCrop"]) < 1e-5
         assert rel_l2(out["pupil"][b], ref["pupil"]) < 1e-5
+
+
+def test_config5_geometry_np1024_l4096():
+    """BASELINE config 5 geometry (Np 1024, L 4096, naRadius 333 -- mono
+    optics at Np 1024): the general path and the batched L = 4096 objCrop
+    transform at full size, 6 LEDs of a synthetic grid, 1 iteration, fp32
+    storage (the fp16-storage variant of config 5 is not built)."""
+    import oracle_lib
+    from tools.synth import grid_geometry
+    Np, L, r = 1024, 4096, 333
+    x0, y0, order = grid_geometry(Np, L, 3, 40)
+    x0, y0 = x0[:6], y0[:6]
+    order = np.arange(6, dtype=np.int32)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=13)
+    ref = oracle_lib.run_fpm(stack[:, 0], order, x0, y0, Np, L, r, 5, 10, 1)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=1)
+    out = fpm_amd.run_fpm(prob, stack, 1)
+    for k in ("objCrop", "objF", "pupil"):
+        e = rel_l2(out[k][0], ref[k])
+        assert e < 1e-5, (k, e)
