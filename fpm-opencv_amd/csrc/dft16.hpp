@@ -88,7 +88,12 @@ __device__ __forceinline__ int opaque_int(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+// read base of lane t, laundered (see above); computed once per kernel
+__device__ __forceinline__ int exch_rbase(int t) { return opaque_int(t * XP); }
+// (a lane-major tile with eight 16-byte writes per lane was measured: pass B
+// +3%, the strided reads cost more than the halved write count saves)
 __device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
+    (void)t;
 #pragma unroll
     for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
 #pragma unroll

@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
-    const int xrd = opaque_int(t * XP);  // exchange read base, see exchange16
+    const int xrd = exch_rbase(t);  // exchange read base, see exchange16
     const int lane = tid & 63, w = tid >> 6;
 #ifdef FPM_EXP_PRIO
     if (w >= NT / 128) __builtin_amdgcn_s_setprio(1);  // second-dispatched half wins arbitration

@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(16 * G) k_crop_rows(const float2 *__restrict__
     float2 *twL = sm;                  // L
     float2 *scr_all = sm + L;          // G exchange tiles
     const int g = threadIdx.x >> 4, t = threadIdx.x & 15;
-    const int xrd = opaque_int(t * XP);
+    const int xrd = exch_rbase(t);
     float2 *scr = scr_all + g * XTILE;
     float2 wt[16];
     load_twiddles(twL, tw_L, L, M, wt, t);
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
     float2 *scr_all = strip;           // G exchange tiles, inside the strip: used
                                        // only while every column is in registers
     const int g = threadIdx.x >> 4, t = threadIdx.x & 15;
-    const int xrd = opaque_int(t * XP);
+    const int xrd = exch_rbase(t);
     float2 *scr = scr_all + g * XTILE;
     float2 wt[16];
     load_twiddles(twL, tw_L, L, M, wt, t);
@@ -177,8 +177,9 @@ template <int M, int GR, int G>
 hipError_t launch_crop(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
     constexpr int L = 256 * M;
     const size_t lds_rows = (size_t)(L + GR * XTILE) * sizeof(float2);
-    static_assert(G * XTILE <= L / 2 * (G + 1), "exchange tiles must fit in the half strip");
-    const size_t lds_cols = (size_t)(L + L / 2 * (G + 1)) * sizeof(float2);
+    // the exchange tiles alias the half strip: allocate the larger of the two
+    constexpr size_t strip = (size_t)L / 2 * (G + 1) > (size_t)G * XTILE ? (size_t)L / 2 * (G + 1) : (size_t)G * XTILE;
+    const size_t lds_cols = (L + strip) * sizeof(float2);
     hipError_t e = hipFuncSetAttribute((const void *)k_crop_rows<M, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds_rows);
     if (e != hipSuccess) return e;
