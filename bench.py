@@ -15,6 +15,8 @@ time).  Launch: `python bench.py` (1 GPU) or torch.distributed.run with
 --nproc-per-node N (one rank per GPU, RCCL).  After the timed region, ranks
 > 0 send their objCrop tiles to rank 0 with one RCCL gather (the stitched-field
 exchange of SURVEY.md 8(e)); its time is reported separately, not in value.
+`--backend gloo` rehearses the N > 1 path (barrier, max-over-ranks timing,
+gather) with several ranks sharing one GPU; bench numbers use nccl (RCCL).
 """
 from __future__ import annotations
 
@@ -100,6 +102,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path with several ranks on one GPU (CPU collectives)")
     ap.add_argument("--data", default="model", choices=["model", "random"],
                     help="random: uniform uint16 stack (profiling runs only; not a bench number)")
     args = ap.parse_args()
@@ -113,9 +117,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPUs (use --backend gloo to rehearse)")
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
+    cdev = torch.device("cuda", local) if args.backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     geo = metric_geometry(args.np)
     B = args.patches
@@ -157,7 +169,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
@@ -182,6 +194,7 @@ def main():
         mine = torch.empty((B, L, L, 2), dtype=torch.float32, device="cuda")
         solver.download_objcrop_device(mine.data_ptr())
         torch.cuda.synchronize()
+        mine = mine.to(cdev)
         dist.barrier()
         g0 = time.perf_counter()
         from fpm_amd import parallel
