@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     __syncthreads();
 
     // diagnostic: shader-clock cycles per phase, summed over LEDs (wave-uniform)
-    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // phases: see api.cpp stamp names
+    unsigned long long acc[kStamps] = {};  // phases: see api.cpp stamp names
     unsigned long long prev = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
 #define FPM_STAMP(i)                                                  \
     if (a.dbg) {                                                      \
@@ -475,6 +475,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                     F[j][s] = cadd(Fp[j][s], o[s]);
                 }
             }
+            FPM_STAMP(8)
             for (int pp = g; pp < a.n_tail_px; pp += NG) {  // tail pixels: 16 lanes sum 128 terms
                 const int2 px = tpx[pp];
                 const float2 *row = th + sig[px.x + KYOFF] * TLD;
@@ -631,7 +632,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     }
 #undef FPM_STAMP
     if (a.dbg && tid == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd(&a.dbg[i], acc[i]);
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[i], acc[i]);
 
     // ---- write back the per-patch state
 #pragma unroll
