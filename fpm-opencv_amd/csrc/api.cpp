@@ -463,8 +463,8 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipMemset(c->dbg, 0, sizeof h));
         const double steps = (double)iters * c->prob.n_order * c->st.B;
         fprintf(stderr, "[fpm stamps] cycles per LED step (wave 0 view, mean over blocks):");
-        const char *names[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "update",
-                                      "max",    "P",           "A:rowIDFT", "C:rowDFT"};
+        const char *names[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre",
+                                      "max",    "P",           "A:rowIDFT", "C:rowDFT",    "upd:body"};
         for (int i = 0; i < kStamps; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / steps);
         fprintf(stderr, "\n");
     }

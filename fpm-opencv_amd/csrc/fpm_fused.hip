@@ -222,9 +222,6 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
     const int xrd = exch_rbase(t);  // exchange read base, see exchange16
     const int lane = tid & 63, w = tid >> 6;
-#ifdef FPM_EXP_PRIO
-    if (w >= NT / 128) __builtin_amdgcn_s_setprio(1);  // second-dispatched half wins arbitration
-#endif
     const int b = blockIdx.x;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * XTILE;
@@ -540,6 +537,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             NPt = cscale(cmul(D, cscale(cconj(o), oa)), rip);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
+        FPM_STAMP(9)
         __syncthreads();  // spectrum writes, tile maxima, dirty bits
         if (it + 1 < a.n_order) {
             const float2 *sr = window(it + 1);

@@ -24,7 +24,7 @@
 namespace fpm {
 
 constexpr int kTile = 16;
-constexpr int kStamps = 9;  // FPM_STAMPS phase counters of the fused kernel
+constexpr int kStamps = 10;  // FPM_STAMPS phase counters of the fused kernel
 
 struct DevState {
     float2 *spec;
