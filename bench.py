@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--pcie", action="store_true",
+                    help="also time the host->device stack upload (fpm_upload_stack from host memory); "
+                         "reported beside the line as upload, never in value")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU (CPU collectives)")
     ap.add_argument("--data", default="model", choices=["model", "random"],
@@ -203,6 +206,26 @@ def main():
         gms = (time.perf_counter() - g0) * 1e3
         gather = dict(ms=round(gms, 2), GB_to_rank0=round(mine.numel() * 4 * (world - 1) / 1e9, 3))
 
+    upload = None
+    if args.pcie and rank == 0:
+        # the same stack from pinned host memory through the C ABI's host entry
+        # point (PCIe + the fused-layout permutation), once per reconstruction
+        host_stack = stack.cpu().pin_memory()
+        torch.cuda.synchronize()
+        u0 = time.perf_counter()
+        import ctypes
+        rc = fpm_amd._lib.fpm_upload_stack(solver._h, ctypes.cast(host_stack.data_ptr(),
+                                                                   ctypes.POINTER(ctypes.c_uint16)))
+        torch.cuda.synchronize()
+        us = time.perf_counter() - u0
+        if rc != 0:
+            raise RuntimeError(fpm_amd._lib.fpm_last_error().decode())
+        gb = host_stack.numel() * 2 / 1e9
+        iters_equiv = us / (elapsed / args.steps)
+        upload = dict(s=round(us, 3), GB=round(gb, 2), GBps=round(gb / us, 1),
+                      iterations_equivalent=round(iters_equiv, 1),
+                      led_updates_per_s_incl_upload_1_iteration=round(B * geo["n_led"] / (us + elapsed / args.steps), 1))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -229,6 +252,8 @@ def main():
         }
         if gather:
             out["gather"] = gather
+        if upload:
+            out["upload"] = upload
         print(json.dumps(out), flush=True)
     solver.close()
     if world > 1:
