@@ -142,3 +142,54 @@ def test_unsupported_fused_radius_falls_back_to_general():
         assert s.info().path == fpm_amd.PATH_GENERAL
     with pytest.raises(fpm_amd.FpmError):
         fpm_amd.Solver(fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, path=fpm_amd.PATH_FUSED))
+
+
+@pytest.mark.parametrize("path", [fpm_amd.PATH_GENERAL, fpm_amd.PATH_FUSED])
+def test_iterations_compose_and_runs_are_deterministic(path):
+    """run(2) == run(1); run(1) bit for bit (the state carried between launches
+    -- spectrum, pupil, tile maxima, dirty bits, max|P| -- is complete), and two
+    contexts on the same input give identical bits (no order-dependent atomics)."""
+    Np, L, r = 256, 512, 33
+    x0, y0, order = grid_geometry(Np, L, 3, 24)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=31)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=2, path=path)
+    outs = []
+    for split in (False, True, True):
+        with fpm_amd.Solver(prob) as s:
+            s.upload(stack)
+            s.init()
+            if split:
+                s.run(1)
+                s.run(1)
+            else:
+                s.run(2)
+            outs.append(s.download())
+    for k in ("objF", "objCrop", "pupil"):
+        np.testing.assert_array_equal(outs[0][k], outs[1][k])
+        np.testing.assert_array_equal(outs[1][k], outs[2][k])
+
+
+def test_objcrop_last_only_flag():
+    Np, L, r = 256, 768, 33
+    x0, y0, order = grid_geometry(Np, L, 3, 24)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=32)
+    a = fpm_amd.run_fpm(fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3), stack, 2)
+    b = fpm_amd.run_fpm(fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, flags=fpm_amd.FLAG_OBJCROP_LAST_ONLY),
+                        stack, 2)
+    for k in ("objF", "objCrop", "pupil"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_fused_more_patches_than_cus():
+    """n_patch > 256: the fused grid runs in more than one wave of workgroups."""
+    import oracle_lib
+    Np, L, r, B = 256, 512, 33, 260
+    x0, y0, order = grid_geometry(Np, L, 2, 24)
+    rng = np.random.default_rng(33)
+    stack = rng.integers(0, 30000, (len(x0), B, Np, Np)).astype(np.uint16)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=B, path=fpm_amd.PATH_FUSED)
+    out = fpm_amd.run_fpm(prob, stack, 1)
+    for b in (0, 255, 259):
+        ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, 10, 3, 1)
+        assert rel_l2(out["objCrop"][b], ref["objCrop"]) < 1e-5
+        assert rel_l2(out["pupil"][b], ref["pupil"]) < 1e-5
