@@ -401,6 +401,10 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             FPM_STAMP(1)
 
             // ---- B: columns x in [128h, 128h+128): IDFT, amplitude replacement, DFT (:365-394)
+            // the column's six half-T slots are read one round ahead as well
+            float2 tin[6];
+#pragma unroll
+            for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(0)];
 #pragma unroll 1
             for (int q = 0; q < NQ; ++q) {
                 const int xl = colx(q);
@@ -417,8 +421,13 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-                for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + xl];
+                for (int s = 0; s < 6; ++s) v[SK[s]] = tin[s];
                 idft256_in6(v, r, scr, wt, t, xrd);
+                {
+                    const int xn = colx(q + 1 < NQ ? q + 1 : q);
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
+                }
                 const unsigned iw[16] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w,
                                          i2.x, i2.y, i2.z, i2.w, i3.x, i3.y, i3.z, i3.w};
 #pragma unroll
