@@ -17,6 +17,8 @@
 // nonzero input only on the (2r+1)^2 box and only the box outputs of the
 // forward transform are ever used.  Row passes therefore run on nb = 2r+1 rows,
 // not Np.
+#include <algorithm>
+
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
 
@@ -199,6 +201,8 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
 // kFftRegElems*blockDim without a ping-pong buffer.
 constexpr int kFftThreads = 512;
 constexpr int kFftRegElems = 24;
+// complex values a radix-R in-place pass can lift into registers across the block
+static int fft_pass_capacity(int R) { return kFftRegElems / R * R * kFftThreads; }
 
 template <int R, bool INV>
 __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int lss, int les, int Ns,
@@ -314,6 +318,67 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
     }
 }
 
+// runs the plan's passes in place over a C = 2^lc column tile (element i of
+// column c at buf[i*C + c]); every thread of the block must call it
+template <bool INV>
+__device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, int lc, const float2 *stw) {
+    int Ns = 1;
+    for (int st = 0; st < pl.nstages; ++st) {
+        const int R = pl.radix[st];
+        switch (R) {
+            case 4: fft_inplace_pass<4, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 2: fft_inplace_pass<2, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 3: fft_inplace_pass<3, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            default: fft_inplace_pass<5, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+        }
+        Ns *= R;
+    }
+}
+
+// ---- K2 (tiled) ---------------------------------------------------------------
+// The column pass for C = 2^lc adjacent columns per block: the box rows of T
+// are read as C*8-byte row segments (coalesced), the column IDFT, amplitude
+// replacement and column DFT run in place in one LDS tile, and only the box
+// rows are written back.  grid (Np / C, B), block kFftThreads.
+__global__ void __launch_bounds__(kFftThreads) k_colpass_tiled(DevState st, StepArgs sa, FftPlan pl,
+                                                               const float2 *__restrict__ tw, int lc) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, cm = C - 1;
+    const int x0 = blockIdx.x << lc, b = blockIdx.y;
+    float2 *tile = smem;                       // np * C
+    float2 *stw = smem + (size_t)np * C;       // np twiddles
+    float2 *T = st.T + (size_t)b * nb * np;
+    for (int i = threadIdx.x; i < np; i += kFftThreads) stw[i] = tw[i];
+    for (int i = threadIdx.x; i < np * C; i += kFftThreads) tile[i] = make_float2(0.f, 0.f);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nb * C; idx += kFftThreads) {
+        const int j = idx >> lc, c = idx & cm;
+        const int i = j - r < 0 ? j - r + np : j - r;
+        tile[i * C + c] = T[(size_t)j * np + x0 + c];
+    }
+    __syncthreads();
+    tile_transform<true>(tile, pl, lc, stw);
+    // amplitude replacement, fpmMain.cpp:378-393 (same arithmetic as k_colpass)
+    const float inv_n2 = 1.0f / ((float)np * (float)np);
+    const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
+    for (int idx = threadIdx.x; idx < np * C; idx += kFftThreads) {
+        const int y = idx >> lc, c = idx & cm;
+        const float2 psi = cscale(tile[idx], inv_n2);
+        const float a = sqrtf((float)I[(size_t)y * np + x0 + c]);
+        const float tre = psi.x + st.eps;
+        const float mag = sqrtf(tre * tre + psi.y * psi.y);
+        const float sc = a / mag;
+        tile[idx] = make_float2(psi.x * sc, psi.y * sc);
+    }
+    __syncthreads();
+    tile_transform<false>(tile, pl, lc, stw);
+    for (int idx = threadIdx.x; idx < nb * C; idx += kFftThreads) {
+        const int j = idx >> lc, c = idx & cm;
+        const int i = j - r < 0 ? j - r + np : j - r;
+        T[(size_t)j * np + x0 + c] = tile[i * C + c];
+    }
+}
+
 // sqrt of the init image as complex, fpmMain.cpp:319-322. grid (Np, B)
 __global__ void k_init_amp(const uint16_t *__restrict__ meas, float2 *__restrict__ out, int np, int B,
                            int led, size_t out_bs) {
@@ -354,6 +419,13 @@ __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
 }
 
 // ---- host-side launchers ----------------------------------------------------
+// C = 2^lc sequences of pl.n fit the in-place transform's register budget
+static bool fft_fits(const FftPlan &pl, int lc) {
+    for (int i = 0; i < pl.nstages; ++i)
+        if ((pl.n << lc) > fft_pass_capacity(pl.radix[i])) return false;
+    return true;
+}
+
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
                                const float2 *tw, hipStream_t s) {
     StepArgs sa;
@@ -362,7 +434,16 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     sa.yc = y0 + st.np / 2;
     const size_t lds = 2 * (size_t)st.np * sizeof(float2);
     hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
-    hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    // tiled column pass when the columns divide into 16-wide tiles that fit
+    // the in-place register-lifted transform; one column per block otherwise
+    int lc = 4;
+    while (lc > 0 && ((st.np & ((1 << lc) - 1)) || !fft_fits(pl, lc))) --lc;
+    if (lc > 0) {
+        const size_t ldt = ((size_t)st.np * (1 << lc) + st.np) * sizeof(float2);
+        hipLaunchKernelGGL(k_colpass_tiled, dim3(st.np >> lc, st.B), dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
+    } else {
+        hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    }
     hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     hipLaunchKernelGGL(k_pupil_commit, dim3(st.B), dim3(1024), 0, s, st, sa);
     return hipGetLastError();
@@ -371,15 +452,14 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
 // largest C = 2^lc with C*n complex values in registers across the block
 // (kFftRegElems per thread; radix-5 passes hold 20) and at most 16 sequences
 int fft_log2_seq_per_block(const FftPlan &pl) {
-    bool has5 = false;
-    for (int i = 0; i < pl.nstages; ++i) has5 |= pl.radix[i] == 5;
-    const int cap = (has5 ? 20 : kFftRegElems) * kFftThreads;
+    int cap = kFftRegElems * kFftThreads;
+    for (int i = 0; i < pl.nstages; ++i) cap = std::min(cap, fft_pass_capacity(pl.radix[i]));
     int lc = 0;
     while (lc < 4 && (pl.n << (lc + 1)) <= cap) ++lc;
     return (pl.n << lc) <= cap ? lc : -1;
 }
 
-int fft_max_len() { return 20 * kFftThreads; }
+int fft_max_len() { return fft_pass_capacity(5); }  // the smallest of the radix-2/3/4/5 capacities
 
 hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
                             int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
