@@ -114,6 +114,10 @@ struct fpm_ctx {
     std::vector<hipEvent_t> evpool;
     unsigned long long *dbg = nullptr;  // FPM_STAMPS=1: fused-kernel phase cycles
     fpm_timing timing{};
+    // general path: one iteration's 4*n_order launches captured once and
+    // replayed as a single graph launch (FPM_NO_GRAPH=1 launches them directly)
+    hipGraph_t led_graph = nullptr;
+    hipGraphExec_t led_graph_exec = nullptr;
 };
 
 namespace {
@@ -131,6 +135,10 @@ int dalloc(fpm_ctx *c, T **p, size_t count) {
 }
 
 void free_all(fpm_ctx *c) {
+    if (c->led_graph_exec) (void)hipGraphExecDestroy(c->led_graph_exec);
+    if (c->led_graph) (void)hipGraphDestroy(c->led_graph);
+    c->led_graph_exec = nullptr;
+    c->led_graph = nullptr;
     for (void *p : c->allocs) (void)hipFree(p);
     c->allocs.clear();
     for (auto e : c->evpool) (void)hipEventDestroy(e);
@@ -407,6 +415,40 @@ int fpm_init(fpm_ctx *c) {
     return FPM_OK;
 }
 
+namespace {
+
+hipError_t launch_general_iteration(fpm_ctx *c, hipStream_t s) {
+    for (int i = 0; i < c->prob.n_order; ++i) {
+        const int led = c->order[i];
+        hipError_t e = launch_general_step(c->st, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// The general path issues four launches per LED (~1200 per iteration at 293
+// LEDs); every argument is fixed once the context exists, so one iteration is
+// captured on the context's own stream and replayed on c->stream.
+int general_graph(fpm_ctx *c) {
+    if (c->led_graph_exec) return FPM_OK;
+    hipStream_t cs = c->own_stream;
+    HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    hipError_t e = launch_general_iteration(c, cs);
+    hipGraph_t g = nullptr;
+    hipError_t e2 = hipStreamEndCapture(cs, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&c->led_graph_exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        c->led_graph_exec = nullptr;
+        return set_err(FPM_ERR_DEVICE, "general-path graph capture: %s", hipGetErrorString(e));
+    }
+    c->led_graph = g;
+    return FPM_OK;
+}
+
+}  // namespace
+
 int fpm_run(fpm_ctx *c, int iters) {
     if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
     if (!c->initialized) return set_err(FPM_ERR_STATE, "fpm_run before fpm_init");
@@ -421,6 +463,11 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventCreate(&e));
         c->evpool.push_back(e);
     }
+    const bool use_graph = c->path != FPM_PATH_FUSED && iters > 0 && !getenv("FPM_NO_GRAPH");
+    if (use_graph) {
+        const int r = general_graph(c);
+        if (r != FPM_OK) return r;
+    }
     hipEvent_t *ev = c->evpool.data();
     HIP_TRY(hipEventRecord(ev[0], c->stream));
     for (int it = 0; it < iters; ++it) {
@@ -428,11 +475,10 @@ int fpm_run(fpm_ctx *c, int iters) {
         if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->dbg, c->stream));
+        } else if (use_graph) {
+            HIP_TRY(hipGraphLaunch(c->led_graph_exec, c->stream));
         } else {
-            for (int i = 0; i < c->prob.n_order; ++i) {
-                const int led = c->order[i];
-                HIP_TRY(launch_general_step(c->st, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, c->stream));
-            }
+            HIP_TRY(launch_general_iteration(c, c->stream));
         }
         HIP_TRY(hipEventRecord(ev[2 + 3 * it], c->stream));
         if (!last_only || it == iters - 1) {
