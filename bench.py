@@ -81,20 +81,40 @@ def load_pmc(path, launch_kernel):
         return None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(geo, stack_host, threads):
     """C++ fp64 reference-faithful restatement (oracle/liboracle.so, 'port'),
-    one patch per thread, all 293 LEDs, one iteration; wall-clock."""
+    one patch per thread, all LEDs, one iteration; wall-clock.  SURVEY.md 8(d)
+    asks for the rate on all host cores (one patch per thread, patches are
+    independent) and on one core: both are measured, `value` is the former."""
     import numpy as np
     import oracle_lib
     order = np.arange(geo["n_led"], dtype=np.int32)
-    t0 = time.perf_counter()
-    oracle_lib.run_fpm_batch(stack_host, order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"],
-                             geo["d1"], geo["d2"], 1, threads, outputs=False)
-    dt = time.perf_counter() - t0
+
+    def timed(stk, nthr):
+        t0 = time.perf_counter()
+        oracle_lib.run_fpm_batch(stk, order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"],
+                                 geo["d1"], geo["d2"], 1, nthr, outputs=False)
+        return time.perf_counter() - t0
+
+    dt = timed(stack_host, threads)
+    dt1 = timed(np.ascontiguousarray(stack_host[:, :1]), 1)
     B = stack_host.shape[1]
-    return dict(value=B * geo["n_led"] / dt, unit="LED-updates/s", cores=threads, kind="port",
+    return dict(value=round(B * geo["n_led"] / dt, 1), unit="LED-updates/s", cores=threads, kind="port",
+                single_core_value=round(geo["n_led"] / dt1, 1), cpu_model=cpu_model(),
                 sample=f"{B} patches x {geo['n_led']} LEDs x 1 iteration, Np={geo['np_']} L={geo['L']}, "
-                       f"complex128, one patch per thread, {dt:.1f} s wall")
+                       f"complex128, one patch per thread on {threads} threads, {dt:.1f} s wall; "
+                       f"single core: 1 patch x {geo['n_led']} LEDs, {dt1:.1f} s")
 
 
 def main():

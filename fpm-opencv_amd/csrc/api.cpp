@@ -24,9 +24,6 @@ namespace fpm {
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
                                const float2 *tw, hipStream_t s);
 int fft_max_len();
-hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
-                            int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
-                            int out_es, int sroll, int iroll, float scale, hipStream_t s);
 hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const FftPlan &pl_np,
                        const float2 *tw_np, hipStream_t s);
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
@@ -205,7 +202,7 @@ extern "C" {
 
 const char *fpm_last_error(void) { return g_err.c_str(); }
 
-const char *fpm_version(void) { return "libfpm_hip 0.1 (gfx950, fp32 complex state)"; }
+const char *fpm_version(void) { return "libfpm_hip 0.2 (gfx950, fp32 complex state, optional fp16 spectrum storage)"; }
 
 int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if (!out) return set_err(FPM_ERR_INVAL, "null out");
@@ -265,14 +262,25 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
             c->support_px += disk[(size_t)i * nb + j];
         }
 
-    if (prob->path == FPM_PATH_FUSED && !fused_supported(np, r, L))
-        return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d", np, r, L));
-    c->path = (prob->path == FPM_PATH_GENERAL) ? FPM_PATH_GENERAL
-              : fused_supported(np, r, L)     ? FPM_PATH_FUSED
-                                              : FPM_PATH_GENERAL;
+    const bool fp16 = (prob->flags & FPM_FLAG_SPEC_FP16) != 0;
+    if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_supported(np, r, L)))
+        return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
+                            fp16 ? " with fp16 spectrum storage" : ""));
+    c->path = (prob->path == FPM_PATH_GENERAL || fp16) ? FPM_PATH_GENERAL
+              : fused_supported(np, r, L)              ? FPM_PATH_FUSED
+                                                       : FPM_PATH_GENERAL;
+    // fp16 storage scale: 2^-ceil(log2 Np^2) (fpm_state.hpp)
+    int e2 = 0;
+    while ((1ll << e2) < (long long)np * np) ++e2;
+    st.hscale = std::ldexp(1.0f, -e2);
+    st.hinv = std::ldexp(1.0f, e2);
 
     const size_t specn = (size_t)B * L * L;
-    if ((rc = dalloc(c, &st.spec, specn))) return fail(rc);
+    if (fp16) {
+        if ((rc = dalloc(c, &st.spec16, specn))) return fail(rc);
+    } else {
+        if ((rc = dalloc(c, &st.spec, specn))) return fail(rc);
+    }
     if ((rc = dalloc(c, &c->objcrop, specn))) return fail(rc);
     if ((rc = dalloc(c, &st.pupil, (size_t)B * nb * nb))) return fail(rc);
     if ((rc = dalloc(c, &st.tmax, (size_t)B * st.ntx * st.nty))) return fail(rc);
@@ -536,8 +544,17 @@ int fpm_download(fpm_ctx *c, float *objF, float *objCrop, float *pupil, float *s
     if (objF) {
         // spec is centred; objF = fftShift(spec) (fpmMain.cpp:447)
         std::vector<float2> h(ll);
+        std::vector<__half2> h16(st.spec16 ? ll : 0);
         for (int b = 0; b < B; ++b) {
-            HIP_TRY(hipMemcpy(h.data(), st.spec + b * ll, ll * sizeof(float2), hipMemcpyDeviceToHost));
+            if (st.spec16) {
+                HIP_TRY(hipMemcpy(h16.data(), st.spec16 + b * ll, ll * sizeof(__half2), hipMemcpyDeviceToHost));
+                for (size_t i = 0; i < ll; ++i) {
+                    const float2 f = __half22float2(h16[i]);
+                    h[i] = make_float2(f.x * st.hinv, f.y * st.hinv);
+                }
+            } else {
+                HIP_TRY(hipMemcpy(h.data(), st.spec + b * ll, ll * sizeof(float2), hipMemcpyDeviceToHost));
+            }
             float2 *o = (float2 *)objF + b * ll;
             for (int y = 0; y < L; ++y)
                 for (int x = 0; x < L; ++x) o[(size_t)y * L + x] = h[(size_t)((y + L / 2) % L) * L + (x + L / 2) % L];

@@ -17,7 +17,14 @@
 //                               max|objF| of fpmMain.cpp:460,467 without an
 //                               L x L pass per LED.
 //   pmax   float  [B]           max |P| (fpmMain.cpp:415) for the next LED.
+//
+// fp16 storage (FPM_FLAG_SPEC_FP16, BASELINE config 5): the spectrum is held
+// as __half2 [B][L][L] scaled by a power of two, hscale = 2^-ceil(log2 Np^2)
+// (|objF| <= Np^2 max sqrt(I) <= 256 Np^2, so the stored magnitude stays
+// <= 256 < 65504); every kernel loads it into fp32, computes in fp32 and
+// rounds once on the store.  spec is then null and spec16 non-null.
 #pragma once
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,6 +35,7 @@ constexpr int kStamps = 10;  // FPM_STAMPS phase counters of the fused kernel
 
 struct DevState {
     float2 *spec;
+    __half2 *spec16;  // fp16 storage of the spectrum (spec == nullptr then)
     float2 *pupil;
     const uint16_t *meas;
     float2 *T;        // [B][nb][Np] row-transform scratch (general path)
@@ -38,6 +46,24 @@ struct DevState {
     const uint8_t *disk;  // [nb][nb] support mask
     int np, L, r, nb, B, ntx, nty;
     float delta1, delta2, eps;
+    float hscale, hinv;  // fp16 storage scale and its inverse (powers of two)
 };
+
+// spectrum element i of patch b (i = y*L + x in the centred spectrum)
+__device__ __forceinline__ float2 spec_ld(const DevState &st, int b, size_t i) {
+    const size_t o = (size_t)b * st.L * st.L + i;
+    if (st.spec16) {
+        const float2 f = __half22float2(st.spec16[o]);
+        return make_float2(f.x * st.hinv, f.y * st.hinv);
+    }
+    return st.spec[o];
+}
+__device__ __forceinline__ void spec_st(const DevState &st, int b, size_t i, float2 v) {
+    const size_t o = (size_t)b * st.L * st.L + i;
+    if (st.spec16)
+        st.spec16[o] = __float22half2_rn(make_float2(v.x * st.hscale, v.y * st.hscale));
+    else
+        st.spec[o] = v;
+}
 
 }  // namespace fpm

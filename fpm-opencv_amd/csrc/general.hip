@@ -38,7 +38,6 @@ __global__ void __launch_bounds__(256) k_gather_rowifft(DevState st, StepArgs sa
     const int row = blockIdx.x, b = blockIdx.y;
     const int ky = row - r;
     float2 *bufa = smem, *bufb = smem + np;
-    const float2 *spec = st.spec + (size_t)b * st.L * st.L;
     const float2 *pup = st.pupil + (size_t)b * nb * nb;
     for (int i = threadIdx.x; i < np; i += blockDim.x) bufa[i] = make_float2(0.f, 0.f);
     __syncthreads();
@@ -46,7 +45,7 @@ __global__ void __launch_bounds__(256) k_gather_rowifft(DevState st, StepArgs sa
     for (int j = threadIdx.x; j < nb; j += blockDim.x) {
         if (st.disk[row * nb + j]) {
             const int kx = j - r;
-            float2 o = spec[(size_t)yrow * st.L + sa.xc + kx];
+            float2 o = spec_ld(st, b, (size_t)yrow * st.L + sa.xc + kx);
             float2 p = pup[row * nb + j];
             bufa[(kx + np) % np] = cmul(o, p);
         }
@@ -102,7 +101,6 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
     for (int i = threadIdx.x; i < np; i += blockDim.x) bufa[i] = T[i];
     __syncthreads();
     float2 *res = stockham<false>(bufa, bufb, 1, pl, tw, threadIdx.x, blockDim.x);
-    float2 *spec = st.spec + (size_t)b * st.L * st.L;
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     float2 *dP = st.dP + (size_t)b * nb * nb;
     const float pm = st.pmax[b];
@@ -111,7 +109,7 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
         if (!st.disk[row * nb + j]) continue;
         const int kx = j - r;
         const size_t si = (size_t)yrow * st.L + sa.xc + kx;
-        const float2 o = spec[si];               // pre-update Objfcrop (:361)
+        const float2 o = spec_ld(st, b, si);     // pre-update Objfcrop (:361)
         const float2 p = pup[row * nb + j];
         const float2 F = res[(kx + np) % np];    // Objfup (:394)
         const float2 D = csub(F, cmul(o, p));    // Objfup - ObjfcropP (:409,463)
@@ -119,7 +117,7 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
         const float pa = cmag(p);
         const float den_o = (pa * pa + st.delta2) * pm;
         const float2 dpc = cmul(D, cscale(cconj(p), pa));
-        spec[si] = make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o);
+        spec_st(st, b, si, make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o));
         // pupil numerator (:459-464,469): D |O| O* / (|O|^2 + d1); max|objF| in K4
         const float oa = cmag(o);
         const float den_p = oa * oa + st.delta1;
@@ -135,7 +133,6 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
     __shared__ float tred[4][4];
     const int r = st.r, nb = st.nb, L = st.L;
     const int b = blockIdx.x;
-    const float2 *spec = st.spec + (size_t)b * L * L;
     float *tmax = st.tmax + (size_t)b * st.nty * st.ntx;
     // 1. refresh the tile maxima under the ROI box (only those pixels changed)
     const int ty0 = (sa.yc - r) / kTile, ty1 = (sa.yc + r) / kTile;
@@ -151,7 +148,7 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
             ty = ty0 + t / ntw;
             tx = tx0 + t % ntw;
             const int y = ty * kTile + (qt >> 4), x = tx * kTile + (qt & 15);
-            if (y < L && x < L) m = cmag(spec[(size_t)y * L + x]);
+            if (y < L && x < L) m = cmag(spec_ld(st, b, (size_t)y * L + x));
         }
         m = wave_max(m);
         if (lane == 0) tred[q][wq] = m;
@@ -257,7 +254,7 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
                                                            const float2 *__restrict__ tw, int lc, int nseq,
                                                            size_t in_bs, int in_ss, int in_es, size_t out_bs,
                                                            int out_ss, int out_es, int sroll, int iroll,
-                                                           float scale) {
+                                                           float scale, const __half2 *in16, float in16_scale) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const int n = pl.n, C = 1 << lc, cm = C - 1;
     const int s0 = blockIdx.x << lc, b = blockIdx.y;
@@ -266,6 +263,7 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
     const int lss = colmajor ? 1 : n + 1, les = colmajor ? C : 1;
     const float rn = 1.0f / (float)n;
     in += (size_t)b * in_bs;
+    if (in16) in16 += (size_t)b * in_bs;
     out += (size_t)b * out_bs;
     const int tot = n << lc;
     // twiddle table in LDS after the tile (a global read per butterfly put an
@@ -290,7 +288,13 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
                 int gs = s0 + sq + sroll, gi = i + iroll;
                 if (gs >= nseq) gs -= nseq;
                 if (gi >= n) gi -= n;
-                v[q] = in[(size_t)gs * in_ss + (size_t)gi * in_es];
+                const size_t ii = (size_t)gs * in_ss + (size_t)gi * in_es;
+                if (in16) {  // fp16-stored spectrum (config 5): widen, undo the storage scale
+                    const float2 f = __half22float2(in16[ii]);
+                    v[q] = make_float2(f.x * in16_scale, f.y * in16_scale);
+                } else {
+                    v[q] = in[ii];
+                }
             }
         }
     }
@@ -394,13 +398,13 @@ __global__ void k_init_place(DevState st, const float2 *__restrict__ F, size_t f
     const int row = blockIdx.x, b = blockIdx.y;
     const int np = st.np, r = st.r, nb = st.nb, L = st.L;
     const int ky = row - r;
-    float2 *spec = st.spec + (size_t)b * L * L;
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     const float2 *f = F + (size_t)b * f_bs;
     for (int j = threadIdx.x; j < nb; j += blockDim.x) {
         const int kx = j - r;
         const bool in = st.disk[row * nb + j];
-        if (in) spec[(size_t)(L / 2 + ky) * L + L / 2 + kx] = f[(size_t)((ky + np) % np) * np + (kx + np) % np];
+        if (in)
+            spec_st(st, b, (size_t)(L / 2 + ky) * L + L / 2 + kx, f[(size_t)((ky + np) % np) * np + (kx + np) % np]);
         pup[row * nb + j] = make_float2(in ? 1.f : 0.f, 0.f);
     }
     if (row == 0 && threadIdx.x == 0) st.pmax[b] = (st.disk[r * nb + r] ? 1.f : 0.f);
@@ -413,7 +417,7 @@ __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
     const int ty = t / st.ntx, tx = t % st.ntx;
     const int y = ty * kTile + (threadIdx.x >> 4), x = tx * kTile + (threadIdx.x & 15);
     float m = 0.f;
-    if (y < L && x < L) m = cmag(st.spec[(size_t)b * L * L + (size_t)y * L + x]);
+    if (y < L && x < L) m = cmag(spec_ld(st, b, (size_t)y * L + x));
     m = block_max(m, red);
     if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = m;
 }
@@ -463,7 +467,8 @@ int fft_max_len() { return fft_pass_capacity(5); }  // the smallest of the radix
 
 hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
                             int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
-                            int out_es, int sroll, int iroll, float scale, hipStream_t s) {
+                            int out_es, int sroll, int iroll, float scale, hipStream_t s,
+                            const __half2 *in16 = nullptr, float in16_scale = 1.f) {
     const int lc = fft_log2_seq_per_block(pl);
     if (lc < 0) return hipErrorInvalidValue;
     const int C = 1 << lc;
@@ -475,10 +480,10 @@ hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const F
     if (e != hipSuccess) return e;
     if (inverse)
         hipLaunchKernelGGL(k_fft_batch<true>, grid, dim3(kFftThreads), lds, s, in, out, pl, tw, lc, nseq, in_bs,
-                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
+                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale, in16, in16_scale);
     else
         hipLaunchKernelGGL(k_fft_batch<false>, grid, dim3(kFftThreads), lds, s, in, out, pl, tw, lc, nseq, in_bs,
-                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale);
+                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale, in16, in16_scale);
     return hipGetLastError();
 }
 
@@ -493,7 +498,8 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
     if (e != hipSuccess) return e;
     e = launch_fft_batch(false, scratch, scratch, pl_np, tw_np, np, st.B, bs, 1, np, bs, 1, np, 0, 0, 1.f, s);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(st.spec, 0, (size_t)st.B * st.L * st.L * sizeof(float2), s);
+    e = st.spec16 ? hipMemsetAsync(st.spec16, 0, (size_t)st.B * st.L * st.L * sizeof(__half2), s)
+                  : hipMemsetAsync(st.spec, 0, (size_t)st.B * st.L * st.L * sizeof(float2), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_init_place, dim3(st.nb, st.B), dim3(256), 0, s, st, (const float2 *)scratch, bs);
     hipLaunchKernelGGL(k_tile_max_all, dim3(st.ntx * st.nty, st.B), dim3(256), 0, s, st);
@@ -509,12 +515,14 @@ hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
                           hipStream_t s) {
     // L = 512 / 768 / 1024: register-resident transforms (objcrop.hip)
-    const hipError_t r = launch_objcrop_regs(st, out, tw_L, s);
-    if (r != hipErrorNotSupported) return r;
+    if (!st.spec16) {
+        const hipError_t r = launch_objcrop_regs(st, out, tw_L, s);
+        if (r != hipErrorNotSupported) return r;
+    }
     const int L = st.L;
     const size_t bs = (size_t)L * L;
     hipError_t e = launch_fft_batch(true, st.spec, out, pl_L, tw_L, L, st.B, bs, L, 1, bs, L, 1, L / 2, L / 2, 1.f,
-                                    s);
+                                    s, st.spec16, st.hinv);
     if (e != hipSuccess) return e;
     return launch_fft_batch(true, out, out, pl_L, tw_L, L, st.B, bs, 1, L, bs, 1, L, 0, 0,
                             1.0f / ((float)L * (float)L), s);

@@ -30,6 +30,7 @@ FPM_ERR_NODEV = -19
 
 PATH_AUTO, PATH_GENERAL, PATH_FUSED = 0, 1, 2
 FLAG_OBJCROP_LAST_ONLY = 1
+FLAG_SPEC_FP16 = 2          # fp16 spectrum storage, fp32 arithmetic (config 5)
 
 # every symbol include/fpm_hip.h declares
 HIP_SYMBOLS = (

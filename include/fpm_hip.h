@@ -69,6 +69,12 @@ typedef struct fpm_frames {
                                           iteration of fpm_run (the reference
                                           recomputes it every iteration,
                                           fpmMain.cpp:481; default keeps that) */
+#define FPM_FLAG_SPEC_FP16         2u  /* store the high-resolution spectrum as
+                                          fp16 (scaled by a power of two), compute
+                                          in fp32: BASELINE config 5 ("fp16
+                                          storage / fp32 accumulate"); general
+                                          path only.  The reference keeps
+                                          CV_64FC2 objF (fpmMain.h:92) */
 
 /*
  * Problem description: the FPM_Dataset fields runFPM reads
