@@ -50,6 +50,42 @@ def metric_geometry(np_=256, max_na=0.6):
                 order_leds=ds.order(), x0=x0, y0=y0)
 
 
+WORKLOADS = {
+    "metric": "dataset_dogStomach optics, 293 LEDs (maxIlluminationNA 0.6), Np=256, L=768, naRadius 33, "
+              "one runFPM iteration per step",
+    "c3": "dataset_dogStomach.json literal (Np=200, maxIlluminationNA 0.4: 157 LEDs, L=600, naRadius 26), "
+          "one runFPM iteration per step",
+    "c5": "config 5: Np=1024, L=4096 spectrum in fp16, naRadius 333, 512-LED synthetic grid, "
+          "one runFPM iteration per step",
+}
+
+
+def config_geometry(name, np_=256):
+    """Geometry of the workload `name` (BASELINE.json configs):
+      metric  configs[1]-style headline: dogStomach optics, Np 256, 293 LEDs
+      c3      configs[2] literal dataset_dogStomach.json: Np 200, maxNA 0.4 ->
+              L 600, naRadius 26, 157 LEDs (general path, mixed radix)
+      c5      configs[4]: Np 1024, L 4096, naRadius 333 (mono optics at
+              Np 1024), 512 LEDs of a synthetic square grid
+              (23 x 23 at a 128-px k-space pitch, the 512 nearest the centre),
+              fp16 spectrum storage
+    Only `metric` is the headline bench line; the others are measured for
+    DESIGN.md."""
+    if name == "metric":
+        return metric_geometry(np_)
+    if name == "c3":
+        return metric_geometry(200, max_na=0.4)
+    if name == "c5":
+        import numpy as np
+        from tools.synth import grid_geometry
+        Np, L = 1024, 4096
+        x0, y0, order = grid_geometry(Np, L, 23, 128)
+        keep = np.array(order[:512])
+        return dict(np_=Np, L=L, r=333, d1=5, d2=10, n_led=512, order_leds=keep,
+                    x0=np.asarray(x0)[keep], y0=np.asarray(y0)[keep])
+    raise ValueError(name)
+
+
 def algorithmic_flops_per_update(np_, nb, support_px):
     """Flops of the support-pruned update per LED-update (DESIGN.md 'Roofline'):
     5 N log2 N per executed 1-D DFT (nb row IDFTs, Np column IDFT+DFT pairs, nb
@@ -122,8 +158,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--patches", type=int, default=256, help="patches per GPU")
+    ap.add_argument("--patches", type=int, default=0, help="patches per GPU (0: 256, 8 for --config c5)")
     ap.add_argument("--np", type=int, default=256)
+    ap.add_argument("--config", default="metric", choices=["metric", "c3", "c5"],
+                    help="workload (config_geometry); only 'metric' is the headline line")
+    ap.add_argument("--fp16", action="store_true", help="fp16 spectrum storage (default for --config c5)")
     ap.add_argument("--path", default="auto", choices=["auto", "general", "fused"])
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,8 +198,9 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    geo = metric_geometry(args.np)
-    B = args.patches
+    geo = config_geometry(args.config, args.np)
+    fp16 = args.fp16 or args.config == "c5"
+    B = args.patches if args.patches > 0 else (8 if args.config == "c5" else 256)
     if args.data == "random":
         g = torch.Generator(device="cuda")
         g.manual_seed(rank)
@@ -172,7 +212,8 @@ def main():
     torch.cuda.synchronize()
     path = {"auto": fpm_amd.PATH_AUTO, "general": fpm_amd.PATH_GENERAL, "fused": fpm_amd.PATH_FUSED}[args.path]
     prob = fpm_amd.Problem(geo["np_"], geo["L"], np.arange(geo["n_led"]), geo["x0"], geo["y0"], geo["r"],
-                           geo["d1"], geo["d2"], n_patch=B, path=path)
+                           geo["d1"], geo["d2"], n_patch=B, path=path,
+                           flags=fpm_amd.FLAG_SPEC_FP16 if fp16 else 0)
     solver = fpm_amd.Solver(prob, device=local)
     solver.upload_device(stack.data_ptr())
     solver.synchronize()
@@ -266,7 +307,7 @@ def main():
                       led_updates_per_s_incl_upload_1_iteration=round(B * geo["n_led"] / (us + elapsed / args.steps), 1))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "metric":
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         host_stack = stack[:, :threads].contiguous().cpu().numpy().view(np.uint16)
         cpu = cpu_baseline(geo, host_stack, threads)
@@ -275,11 +316,12 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "LED-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (fp16 spectrum storage)" if fp16 else "f32",
             "data": ("synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16"
                      if args.data == "model" else "random uint16 (profiling only)"),
-            "config": {"workload": "dataset_dogStomach optics, 293 LEDs (maxIlluminationNA 0.6), Np=256, "
-                                   "L=768, naRadius 33, one runFPM iteration per step",
+            "config": {"workload": WORKLOADS[args.config] if args.np == 256 or args.config != "metric" else
+                                   f"dogStomach optics, Np={geo['np_']}, one runFPM iteration per step",
                        "patches_per_gpu": B, "leds": int(geo["n_led"]), "np": int(geo["np_"]),
                        "nlarge": int(geo["L"]), "na_radius": int(geo["r"]),
                        "path": "fused" if info.path == fpm_amd.PATH_FUSED else "general",

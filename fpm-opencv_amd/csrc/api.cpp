@@ -24,6 +24,7 @@ namespace fpm {
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
                                const float2 *tw, hipStream_t s);
 int fft_max_len();
+int pupil_parts(int nb);
 hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const FftPlan &pl_np,
                        const float2 *tw_np, hipStream_t s);
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
@@ -285,7 +286,8 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &st.pupil, (size_t)B * nb * nb))) return fail(rc);
     if ((rc = dalloc(c, &st.tmax, (size_t)B * st.ntx * st.nty))) return fail(rc);
     if ((rc = dalloc(c, &st.tdirty, (size_t)B * ((st.ntx * st.nty + 31) / 32)))) return fail(rc);
-    if ((rc = dalloc(c, &st.pmax, (size_t)B))) return fail(rc);
+    st.npart = (c->path == FPM_PATH_GENERAL) ? pupil_parts(nb) : 1;
+    if ((rc = dalloc(c, &st.pmax, (size_t)B * st.npart))) return fail(rc);
     if ((rc = dalloc(c, &c->disk_dev, disk.size()))) return fail(rc);
     if ((rc = dalloc(c, &c->meas, (size_t)prob->n_stack * B * np * np))) return fail(rc);
     if ((rc = dalloc(c, &c->order_dev, (size_t)prob->n_order))) return fail(rc);
@@ -294,6 +296,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if (c->path == FPM_PATH_GENERAL) {
         if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
+        if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
     } else {
         if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(float))))
             return fail(rc);

@@ -16,7 +16,11 @@
 //   tmax   float  [B][nty][ntx] max |spec| per 16x16 tile: the exact global
 //                               max|objF| of fpmMain.cpp:460,467 without an
 //                               L x L pass per LED.
-//   pmax   float  [B]           max |P| (fpmMain.cpp:415) for the next LED.
+//   rmax   float  [B][nty]      general path: max of tmax over each tile row,
+//                               so max|objF| is a max over nty values.
+//   pmax   float  [B][npart]    max |P| (fpmMain.cpp:415) for the next LED, as
+//                               npart partial maxima (one per pupil-commit
+//                               block of the general path; npart = 1 fused).
 //
 // fp16 storage (FPM_FLAG_SPEC_FP16, BASELINE config 5): the spectrum is held
 // as __half2 [B][L][L] scaled by a power of two, hscale = 2^-ceil(log2 Np^2)
@@ -42,9 +46,11 @@ struct DevState {
     float2 *dP;       // [B][nb][nb] pupil-update numerator (general path)
     float *tmax;      // [B][nty][ntx]
     unsigned *tdirty; // [B][ceil(ntx*nty/32)] fused path: tiles whose max is an upper bound
-    float *pmax;      // [B]
+    float *rmax;      // [B][nty] general path: row maxima of tmax
+    float *pmax;      // [B][npart]
     const uint8_t *disk;  // [nb][nb] support mask
     int np, L, r, nb, B, ntx, nty;
+    int npart;        // partial max|P| values per patch
     float delta1, delta2, eps;
     float hscale, hinv;  // fp16 storage scale and its inverse (powers of two)
 };

@@ -9,9 +9,13 @@
 //   K3 k_rowfft_update    row DFT of the box rows, object update written to
 //                         the centred spectrum, pupil-update numerator
 //                                                   (fpmMain.cpp:394-447,457-464)
-//   K4 k_pupil_commit     tile maxima of |spec| under the ROI -> exact
-//                         max|objF|, P += num/max * S, max|P| for the next LED
-//                                                   (fpmMain.cpp:459-475,415)
+//   K4 k_tile_rows        tile maxima of |spec| under the ROI and the maxima
+//                         of those tile rows                (fpmMain.cpp:460,467)
+//   K5 k_pupil_commit     exact max|objF| from the row maxima, P += num/max * S
+//                         on a slice of the support box, partial max|P| for
+//                         the next LED                       (fpmMain.cpp:459-475,415)
+// K4 and K5 spread one patch over many workgroups, so a context with a few
+// large patches (config 5: Np 1024, L 4096) still fills the chip.
 //
 // Pruning: P vanishes outside the support disk, so the inverse transform has
 // nonzero input only on the (2r+1)^2 box and only the box outputs of the
@@ -103,7 +107,12 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
     float2 *res = stockham<false>(bufa, bufb, 1, pl, tw, threadIdx.x, blockDim.x);
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     float2 *dP = st.dP + (size_t)b * nb * nb;
-    const float pm = st.pmax[b];
+    // max|P| of the previous commit: the block reads the npart partial maxima
+    // in parallel (a serial scalar-load chain cost ~30 us at npart ~ 100)
+    __shared__ float red[4];
+    float pm = 0.f;
+    for (int i = threadIdx.x; i < st.npart; i += blockDim.x) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
+    pm = block_max(pm, red);
     const int yrow = sa.yc + ky;
     for (int j = threadIdx.x; j < nb; j += blockDim.x) {
         if (!st.disk[row * nb + j]) continue;
@@ -127,48 +136,60 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
 }
 
 // ---- K4 ---------------------------------------------------------------------
-// grid (B), block 1024
-__global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa) {
-    __shared__ float red[32];
-    __shared__ float tred[4][4];
-    const int r = st.r, nb = st.nb, L = st.L;
-    const int b = blockIdx.x;
-    float *tmax = st.tmax + (size_t)b * st.nty * st.ntx;
-    // 1. refresh the tile maxima under the ROI box (only those pixels changed)
-    const int ty0 = (sa.yc - r) / kTile, ty1 = (sa.yc + r) / kTile;
+// grid (ROI tile rows, B), block 256: one tile row of the ROI box per block.
+// Each wave refreshes whole 16x16 tiles (4 pixels per lane, no barrier); the
+// block then folds the row's other (unchanged) tile maxima into rmax.
+constexpr int kRowThreads = 256;
+__global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs sa) {
+    __shared__ float red[kRowThreads / 64];
+    extern __shared__ float fresh[];  // the ROI's tiles of this row
+    const int r = st.r, L = st.L, ntx = st.ntx;
+    const int b = blockIdx.y;
+    const int ty = (sa.yc - r) / kTile + blockIdx.x;
     const int tx0 = (sa.xc - r) / kTile, tx1 = (sa.xc + r) / kTile;
-    const int ntw = tx1 - tx0 + 1, nt = (ty1 - ty0 + 1) * ntw;
-    const int q = threadIdx.x >> 8, qt = threadIdx.x & 255;
-    const int lane = threadIdx.x & 63, wq = (threadIdx.x >> 6) & 3;
-    for (int t0 = 0; t0 < nt; t0 += 4) {
-        const int t = t0 + q;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float *tmax = st.tmax + (size_t)b * st.nty * ntx + (size_t)ty * ntx;
+    for (int tx = tx0 + w; tx <= tx1; tx += kRowThreads / 64) {
         float m = 0.f;
-        int ty = 0, tx = 0;
-        if (t < nt) {
-            ty = ty0 + t / ntw;
-            tx = tx0 + t % ntw;
-            const int y = ty * kTile + (qt >> 4), x = tx * kTile + (qt & 15);
-            if (y < L && x < L) m = cmag(spec_ld(st, b, (size_t)y * L + x));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = lane + 64 * j;
+            const int y = ty * kTile + (p >> 4), x = tx * kTile + (p & 15);
+            if (y < L && x < L) m = fmaxf(m, cmag(spec_ld(st, b, (size_t)y * L + x)));
         }
         m = wave_max(m);
-        if (lane == 0) tred[q][wq] = m;
-        __syncthreads();
-        if (t < nt && qt == 0)
-            tmax[ty * st.ntx + tx] = fmaxf(fmaxf(tred[q][0], tred[q][1]), fmaxf(tred[q][2], tred[q][3]));
-        __syncthreads();
+        if (lane == 0) {
+            tmax[tx] = m;
+            fresh[tx - tx0] = m;
+        }
     }
-    // make this block's tile writes visible to its own later loads
-    __threadfence_block();
     __syncthreads();
-    // 2. global max|objF| (fpmMain.cpp:467)
+    // the refreshed tiles come from LDS, the rest of the row is unchanged
     float m = 0.f;
-    for (int i = threadIdx.x; i < st.ntx * st.nty; i += blockDim.x) m = fmaxf(m, tmax[i]);
+    for (int tx = threadIdx.x; tx < ntx; tx += kRowThreads)
+        m = fmaxf(m, (tx >= tx0 && tx <= tx1) ? fresh[tx - tx0] : tmax[tx]);
+    m = block_max(m, red);
+    if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = m;
+}
+
+// ---- K5 ---------------------------------------------------------------------
+// grid (npart, B), block 256: global max|objF| (fpmMain.cpp:467) from the nty
+// row maxima, then P += num / max * S (fpmMain.cpp:470-475) on this block's
+// slice of the support box and its partial max|P| for the next LED (:415).
+constexpr int kCommitThreads = 256;
+__global__ void __launch_bounds__(kCommitThreads) k_pupil_commit(DevState st) {
+    __shared__ float red[kCommitThreads / 64];
+    const int nb = st.nb, b = blockIdx.y, part = blockIdx.x;
+    const float *rmax = st.rmax + (size_t)b * st.nty;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < st.nty; i += kCommitThreads) m = fmaxf(m, rmax[i]);
     const float omax = block_max(m, red);
-    // 3. P += num / max * S (fpmMain.cpp:470-475); 4. max|P| for the next LED
+    const int n = nb * nb, chunk = (n + st.npart - 1) / st.npart;
+    const int i0 = part * chunk, i1 = min(n, i0 + chunk);
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     const float2 *dP = st.dP + (size_t)b * nb * nb;
     float pm = 0.f;
-    for (int i = threadIdx.x; i < nb * nb; i += blockDim.x) {
+    for (int i = i0 + threadIdx.x; i < i1; i += kCommitThreads) {
         if (!st.disk[i]) continue;
         float2 p = pup[i];
         const float2 d = dP[i];
@@ -178,8 +199,12 @@ __global__ void __launch_bounds__(1024) k_pupil_commit(DevState st, StepArgs sa)
         pm = fmaxf(pm, cmag(p));
     }
     pm = block_max(pm, red);
-    if (threadIdx.x == 0) st.pmax[b] = pm;
+    if (threadIdx.x == 0) st.pmax[b * st.npart + part] = pm;
 }
+
+// support-box pixels per K5 block
+constexpr int kCommitPx = 4096;
+int pupil_parts(int nb) { return std::max(1, (nb * nb + kCommitPx - 1) / kCommitPx); }
 
 // ---- init / output kernels -------------------------------------------------
 
@@ -407,7 +432,8 @@ __global__ void k_init_place(DevState st, const float2 *__restrict__ F, size_t f
             spec_st(st, b, (size_t)(L / 2 + ky) * L + L / 2 + kx, f[(size_t)((ky + np) % np) * np + (kx + np) % np]);
         pup[row * nb + j] = make_float2(in ? 1.f : 0.f, 0.f);
     }
-    if (row == 0 && threadIdx.x == 0) st.pmax[b] = (st.disk[r * nb + r] ? 1.f : 0.f);
+    // max|P0| = 1 (partial maxima other than part 0 were zeroed by launch_init)
+    if (row == 0 && threadIdx.x == 0) st.pmax[b * st.npart] = (st.disk[r * nb + r] ? 1.f : 0.f);
 }
 
 // tile maxima of |spec| from scratch. grid (ntx*nty, B), block 256
@@ -420,6 +446,17 @@ __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
     if (y < L && x < L) m = cmag(spec_ld(st, b, (size_t)y * L + x));
     m = block_max(m, red);
     if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = m;
+}
+
+// row maxima of the tile maxima from scratch (general path). grid (nty, B)
+__global__ void __launch_bounds__(256) k_row_max_all(DevState st) {
+    __shared__ float red[4];
+    const int ty = blockIdx.x, b = blockIdx.y;
+    const float *tm = st.tmax + ((size_t)b * st.nty + ty) * st.ntx;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < st.ntx; i += 256) m = fmaxf(m, tm[i]);
+    m = block_max(m, red);
+    if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = m;
 }
 
 // ---- host-side launchers ----------------------------------------------------
@@ -449,7 +486,10 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
         hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
     }
     hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
-    hipLaunchKernelGGL(k_pupil_commit, dim3(st.B), dim3(1024), 0, s, st, sa);
+    const int nrow = (sa.yc + st.r) / kTile - (sa.yc - st.r) / kTile + 1;
+    const int ncol = (sa.xc + st.r) / kTile - (sa.xc - st.r) / kTile + 1;
+    hipLaunchKernelGGL(k_tile_rows, dim3(nrow, st.B), dim3(kRowThreads), ncol * sizeof(float), s, st, sa);
+    hipLaunchKernelGGL(k_pupil_commit, dim3(st.npart, st.B), dim3(kCommitThreads), 0, s, st);
     return hipGetLastError();
 }
 
@@ -501,8 +541,11 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
     e = st.spec16 ? hipMemsetAsync(st.spec16, 0, (size_t)st.B * st.L * st.L * sizeof(__half2), s)
                   : hipMemsetAsync(st.spec, 0, (size_t)st.B * st.L * st.L * sizeof(float2), s);
     if (e != hipSuccess) return e;
+    e = hipMemsetAsync(st.pmax, 0, (size_t)st.B * st.npart * sizeof(float), s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_init_place, dim3(st.nb, st.B), dim3(256), 0, s, st, (const float2 *)scratch, bs);
     hipLaunchKernelGGL(k_tile_max_all, dim3(st.ntx * st.nty, st.B), dim3(256), 0, s, st);
+    if (st.rmax) hipLaunchKernelGGL(k_row_max_all, dim3(st.nty, st.B), dim3(256), 0, s, st);
     e = hipMemsetAsync(st.tdirty, 0, (size_t)st.B * ((st.ntx * st.nty + 31) / 32) * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     return hipGetLastError();
