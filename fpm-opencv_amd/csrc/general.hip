@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
 // grid (ROI tile rows, B), block 256: one tile row of the ROI box per block.
 // Each wave refreshes whole 16x16 tiles (4 pixels per lane, no barrier); the
 // block then folds the row's other (unchanged) tile maxima into rmax.
-constexpr int kRowThreads = 256;
+constexpr int kRowThreads = 1024;
 __global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs sa) {
     __shared__ float red[kRowThreads / 64];
     extern __shared__ float fresh[];  // the ROI's tiles of this row
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(kCommitThreads) k_pupil_commit(DevState st) {
 }
 
 // support-box pixels per K5 block
-constexpr int kCommitPx = 4096;
+constexpr int kCommitPx = 1024;
 int pupil_parts(int nb) { return std::max(1, (nb * nb + kCommitPx - 1) / kCommitPx); }
 
 // ---- init / output kernels -------------------------------------------------
@@ -224,9 +224,9 @@ int pupil_parts(int nb) { return std::max(1, (nb * nb + kCommitPx - 1) / kCommit
 constexpr int kFftThreads = 512;
 constexpr int kFftRegElems = 24;
 // complex values a radix-R in-place pass can lift into registers across the block
-static int fft_pass_capacity(int R) { return kFftRegElems / R * R * kFftThreads; }
+static int fft_pass_capacity(int R, int nt = kFftThreads) { return kFftRegElems / R * R * nt; }
 
-template <int R, bool INV>
+template <int R, bool INV, int NT = kFftThreads>
 __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int lss, int les, int Ns,
                                                  const float2 *__restrict__ tw) {
     constexpr int Q = kFftRegElems / R;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int
     int dst[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const int jj = threadIdx.x + q * kFftThreads;
+        const int jj = threadIdx.x + q * NT;
         if (jj < total) {
             const int sq = jj & ((1 << lc) - 1), j = jj >> lc;
             const float2 *src = buf + sq * lss;
@@ -265,7 +265,7 @@ __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const int jj = threadIdx.x + q * kFftThreads;
+        const int jj = threadIdx.x + q * NT;
         if (jj < total) {
 #pragma unroll
             for (int r = 0; r < R; ++r) buf[dst[q] + r * Ns * les] = v[q][r];
@@ -349,18 +349,115 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
 
 // runs the plan's passes in place over a C = 2^lc column tile (element i of
 // column c at buf[i*C + c]); every thread of the block must call it
-template <bool INV>
+template <bool INV, int NT>
 __device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, int lc, const float2 *stw) {
     int Ns = 1;
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
-            case 4: fft_inplace_pass<4, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
-            case 2: fft_inplace_pass<2, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
-            case 3: fft_inplace_pass<3, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
-            default: fft_inplace_pass<5, INV>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 4: fft_inplace_pass<4, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 2: fft_inplace_pass<2, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 3: fft_inplace_pass<3, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            default: fft_inplace_pass<5, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
         }
         Ns *= R;
+    }
+}
+
+// the plan's passes in place over C = 2^lc sequences with arbitrary strides
+// (row tiles: lss = n + 1, les = 1)
+template <bool INV, int NT>
+__device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl, int lc, int lss, int les,
+                                                  const float2 *stw) {
+    int Ns = 1;
+    for (int st = 0; st < pl.nstages; ++st) {
+        const int R = pl.radix[st];
+        switch (R) {
+            case 4: fft_inplace_pass<4, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            case 2: fft_inplace_pass<2, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            case 3: fft_inplace_pass<3, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            default: fft_inplace_pass<5, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
+        }
+        Ns *= R;
+    }
+}
+
+// ---- K1 / K3 (tiled) ------------------------------------------------------------
+// C = 2^lc box rows per block in one row-major LDS tile (pitch Np + 1) with
+// the twiddles beside it: the row transforms of a block run together, in
+// place, instead of one 256-thread block per row with global twiddle reads.
+// grid (ceil(nb / C), B), block NT.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_gather_rowifft_tiled(DevState st, StepArgs sa, FftPlan pl,
+                                                             const float2 *__restrict__ tw, int lc) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = np + 1;
+    const int j0 = blockIdx.x << lc, b = blockIdx.y;
+    const int cs = min(C, nb - j0);
+    float2 *tile = smem, *stw = smem + (size_t)C * lss;
+    const float2 *pup = st.pupil + (size_t)b * nb * nb;
+    for (int i = threadIdx.x; i < np; i += NT) stw[i] = tw[i];
+    for (int i = threadIdx.x; i < C * lss; i += NT) tile[i] = make_float2(0.f, 0.f);
+    __syncthreads();
+    const float rnb = 1.0f / (float)nb;
+    for (int idx = threadIdx.x; idx < cs * nb; idx += NT) {
+        const int c = udiv(idx, nb, rnb), j = idx - c * nb, row = j0 + c;
+        if (!st.disk[row * nb + j]) continue;
+        const int kx = j - r;
+        const float2 o = spec_ld(st, b, (size_t)(sa.yc + row - r) * st.L + sa.xc + kx);  // :358-362
+        tile[c * lss + (kx < 0 ? kx + np : kx)] = cmul(o, pup[row * nb + j]);            // :364
+    }
+    __syncthreads();
+    tile_transform_ex<true, NT>(tile, pl, lc, lss, 1, stw);                              // :365
+    float2 *T = st.T + ((size_t)b * nb + j0) * np;
+    const float rnp = 1.0f / (float)np;
+    for (int idx = threadIdx.x; idx < cs * np; idx += NT) {
+        const int c = udiv(idx, np, rnp), i = idx - c * np;
+        T[(size_t)c * np + i] = tile[c * lss + i];
+    }
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_rowfft_update_tiled(DevState st, StepArgs sa, FftPlan pl,
+                                                            const float2 *__restrict__ tw, int lc) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    __shared__ float red[NT / 64];
+    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = np + 1;
+    const int j0 = blockIdx.x << lc, b = blockIdx.y;
+    const int cs = min(C, nb - j0);
+    float2 *tile = smem, *stw = smem + (size_t)C * lss;
+    for (int i = threadIdx.x; i < np; i += NT) stw[i] = tw[i];
+    const float2 *T = st.T + ((size_t)b * nb + j0) * np;
+    const float rnp = 1.0f / (float)np;
+    for (int idx = threadIdx.x; idx < C * np; idx += NT) {
+        const int c = udiv(idx, np, rnp), i = idx - c * np;
+        tile[c * lss + i] = c < cs ? T[(size_t)c * np + i] : make_float2(0.f, 0.f);
+    }
+    // max|P| of the previous commit from its npart partial maxima
+    float pm = 0.f;
+    for (int i = threadIdx.x; i < st.npart; i += NT) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
+    pm = block_max(pm, red);  // its barriers also publish the tile
+    tile_transform_ex<false, NT>(tile, pl, lc, lss, 1, stw);                             // :394
+    float2 *pup = st.pupil + (size_t)b * nb * nb;
+    float2 *dP = st.dP + (size_t)b * nb * nb;
+    const float rnb = 1.0f / (float)nb;
+    for (int idx = threadIdx.x; idx < cs * nb; idx += NT) {
+        const int c = udiv(idx, nb, rnb), j = idx - c * nb, row = j0 + c;
+        if (!st.disk[row * nb + j]) continue;
+        const int kx = j - r;
+        const size_t si = (size_t)(sa.yc + row - r) * st.L + sa.xc + kx;
+        const float2 o = spec_ld(st, b, si);                    // pre-update Objfcrop (:361)
+        const float2 p = pup[row * nb + j];
+        const float2 F = tile[c * lss + (kx < 0 ? kx + np : kx)];  // Objfup (:394)
+        const float2 D = csub(F, cmul(o, p));                   // Objfup - ObjfcropP (:409,463)
+        const float pa = cmag(p);                               // object update (:406-419,433)
+        const float den_o = (pa * pa + st.delta2) * pm;
+        const float2 dpc = cmul(D, cscale(cconj(p), pa));
+        spec_st(st, b, si, make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o));
+        const float oa = cmag(o);                               // pupil numerator (:459-464,469)
+        const float den_p = oa * oa + st.delta1;
+        const float2 n = cmul(D, cscale(cconj(o), oa));
+        dP[row * nb + j] = make_float2(n.x / den_p, n.y / den_p);
     }
 }
 
@@ -368,30 +465,36 @@ __device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, i
 // The column pass for C = 2^lc adjacent columns per block: the box rows of T
 // are read as C*8-byte row segments (coalesced), the column IDFT, amplitude
 // replacement and column DFT run in place in one LDS tile, and only the box
-// rows are written back.  grid (Np / C, B), block kFftThreads.
-__global__ void __launch_bounds__(kFftThreads) k_colpass_tiled(DevState st, StepArgs sa, FftPlan pl,
-                                                               const float2 *__restrict__ tw, int lc) {
+// rows are written back.  The last tile may be partial (Np not a multiple of
+// C: its missing columns are zero and never stored).  grid (ceil(Np / C), B),
+// block NT (256 when the tile fits its register-lifted passes, so a 16 x 200
+// tile keeps every wave busy instead of idling half of a 512-thread block).
+template <int NT>
+__global__ void __launch_bounds__(NT) k_colpass_tiled(DevState st, StepArgs sa, FftPlan pl,
+                                                      const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, cm = C - 1;
     const int x0 = blockIdx.x << lc, b = blockIdx.y;
+    const int cs = min(C, np - x0);            // columns present in this tile
     float2 *tile = smem;                       // np * C
     float2 *stw = smem + (size_t)np * C;       // np twiddles
     float2 *T = st.T + (size_t)b * nb * np;
-    for (int i = threadIdx.x; i < np; i += kFftThreads) stw[i] = tw[i];
-    for (int i = threadIdx.x; i < np * C; i += kFftThreads) tile[i] = make_float2(0.f, 0.f);
+    for (int i = threadIdx.x; i < np; i += NT) stw[i] = tw[i];
+    for (int i = threadIdx.x; i < np * C; i += NT) tile[i] = make_float2(0.f, 0.f);
     __syncthreads();
-    for (int idx = threadIdx.x; idx < nb * C; idx += kFftThreads) {
+    for (int idx = threadIdx.x; idx < nb * C; idx += NT) {
         const int j = idx >> lc, c = idx & cm;
         const int i = j - r < 0 ? j - r + np : j - r;
-        tile[i * C + c] = T[(size_t)j * np + x0 + c];
+        if (c < cs) tile[i * C + c] = T[(size_t)j * np + x0 + c];
     }
     __syncthreads();
-    tile_transform<true>(tile, pl, lc, stw);
+    tile_transform<true, NT>(tile, pl, lc, stw);
     // amplitude replacement, fpmMain.cpp:378-393 (same arithmetic as k_colpass)
     const float inv_n2 = 1.0f / ((float)np * (float)np);
     const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
-    for (int idx = threadIdx.x; idx < np * C; idx += kFftThreads) {
+    for (int idx = threadIdx.x; idx < np * C; idx += NT) {
         const int y = idx >> lc, c = idx & cm;
+        if (c >= cs) continue;
         const float2 psi = cscale(tile[idx], inv_n2);
         const float a = sqrtf((float)I[(size_t)y * np + x0 + c]);
         const float tre = psi.x + st.eps;
@@ -400,11 +503,11 @@ __global__ void __launch_bounds__(kFftThreads) k_colpass_tiled(DevState st, Step
         tile[idx] = make_float2(psi.x * sc, psi.y * sc);
     }
     __syncthreads();
-    tile_transform<false>(tile, pl, lc, stw);
-    for (int idx = threadIdx.x; idx < nb * C; idx += kFftThreads) {
+    tile_transform<false, NT>(tile, pl, lc, stw);
+    for (int idx = threadIdx.x; idx < nb * C; idx += NT) {
         const int j = idx >> lc, c = idx & cm;
         const int i = j - r < 0 ? j - r + np : j - r;
-        T[(size_t)j * np + x0 + c] = tile[i * C + c];
+        if (c < cs) T[(size_t)j * np + x0 + c] = tile[i * C + c];
     }
 }
 
@@ -461,9 +564,9 @@ __global__ void __launch_bounds__(256) k_row_max_all(DevState st) {
 
 // ---- host-side launchers ----------------------------------------------------
 // C = 2^lc sequences of pl.n fit the in-place transform's register budget
-static bool fft_fits(const FftPlan &pl, int lc) {
+static bool fft_fits(const FftPlan &pl, int lc, int nt = kFftThreads) {
     for (int i = 0; i < pl.nstages; ++i)
-        if ((pl.n << lc) > fft_pass_capacity(pl.radix[i])) return false;
+        if ((pl.n << lc) > fft_pass_capacity(pl.radix[i], nt)) return false;
     return true;
 }
 
@@ -474,18 +577,41 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     sa.xc = x0 + st.np / 2;
     sa.yc = y0 + st.np / 2;
     const size_t lds = 2 * (size_t)st.np * sizeof(float2);
-    hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
-    // tiled column pass when the columns divide into 16-wide tiles that fit
-    // the in-place register-lifted transform; one column per block otherwise
+    // row kernels: up to 16 box rows per block, fewer while a few large
+    // patches would leave the chip short of blocks (one row per block when
+    // not even 2 rows fit a 256-thread tile)
+    int lr = 4;
+    while (lr > 0 && !fft_fits(pl, lr, 256)) --lr;
+    auto rblk = [&](int l) { return ((st.nb + (1 << l) - 1) >> l) * st.B; };
+    while (lr > 1 && rblk(lr) < 512) --lr;
+    const size_t ldr = ((size_t)(st.np + 1) * (1 << lr) + st.np) * sizeof(float2);
+    const dim3 rgrid((st.nb + (1 << lr) - 1) >> lr, st.B);
+    if (lr > 0)
+        hipLaunchKernelGGL(k_gather_rowifft_tiled<256>, rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+    else
+        hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    // tiled column pass: up to 16 columns per block while the tile fits the
+    // in-place register-lifted transform, fewer (down to 4) when a few large
+    // patches would leave the chip short of blocks; one column per block when
+    // not even 2 columns fit
     int lc = 4;
-    while (lc > 0 && ((st.np & ((1 << lc) - 1)) || !fft_fits(pl, lc))) --lc;
+    while (lc > 0 && !fft_fits(pl, lc)) --lc;
+    auto nblk = [&](int l) { return ((st.np + (1 << l) - 1) >> l) * st.B; };
+    while (lc > 2 && nblk(lc) < 512) --lc;
     if (lc > 0) {
         const size_t ldt = ((size_t)st.np * (1 << lc) + st.np) * sizeof(float2);
-        hipLaunchKernelGGL(k_colpass_tiled, dim3(st.np >> lc, st.B), dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
+        const dim3 grid((st.np + (1 << lc) - 1) >> lc, st.B);
+        if (fft_fits(pl, lc, 256))
+            hipLaunchKernelGGL(k_colpass_tiled<256>, grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
+        else
+            hipLaunchKernelGGL(k_colpass_tiled<kFftThreads>, grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
     } else {
         hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
     }
-    hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
+    if (lr > 0)
+        hipLaunchKernelGGL(k_rowfft_update_tiled<256>, rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+    else
+        hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     const int nrow = (sa.yc + st.r) / kTile - (sa.yc - st.r) / kTile + 1;
     const int ncol = (sa.xc + st.r) / kTile - (sa.xc - st.r) / kTile + 1;
     hipLaunchKernelGGL(k_tile_rows, dim3(nrow, st.B), dim3(kRowThreads), ncol * sizeof(float), s, st, sa);

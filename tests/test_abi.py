@@ -51,3 +51,12 @@ def test_create_rejects_bad_problems(change, match):
     with pytest.raises(fpm_amd.FpmError, match=match) as e:
         fpm_amd.Solver(fpm_amd.Problem(**base))
     assert e.value.code == fpm_amd.FPM_ERR_INVAL
+
+
+def test_flag_and_path_constants_match_header():
+    text = open(os.path.join(ROOT, "include", "fpm_hip.h")).read()
+    defs = dict(re.findall(r"#define\s+(FPM_(?:FLAG|PATH)_\w+)\s+(\d+)u?", text))
+    assert int(defs["FPM_FLAG_OBJCROP_LAST_ONLY"]) == fpm_amd.FLAG_OBJCROP_LAST_ONLY
+    assert int(defs["FPM_FLAG_SPEC_FP16"]) == fpm_amd.FLAG_SPEC_FP16
+    assert (int(defs["FPM_PATH_AUTO"]), int(defs["FPM_PATH_GENERAL"]), int(defs["FPM_PATH_FUSED"])) == \
+        (fpm_amd.PATH_AUTO, fpm_amd.PATH_GENERAL, fpm_amd.PATH_FUSED)
