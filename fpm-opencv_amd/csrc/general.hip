@@ -224,12 +224,12 @@ int pupil_parts(int nb) { return std::max(1, (nb * nb + kCommitPx - 1) / kCommit
 constexpr int kFftThreads = 512;
 constexpr int kFftRegElems = 24;
 // complex values a radix-R in-place pass can lift into registers across the block
-static int fft_pass_capacity(int R, int nt = kFftThreads) { return kFftRegElems / R * R * nt; }
+static int fft_pass_capacity(int R, int nt = kFftThreads, int e = kFftRegElems) { return e / R * R * nt; }
 
-template <int R, bool INV, int NT = kFftThreads>
+template <int R, bool INV, int NT = kFftThreads, int E = kFftRegElems>
 __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int lss, int les, int Ns,
                                                  const float2 *__restrict__ tw) {
-    constexpr int Q = kFftRegElems / R;
+    constexpr int Q = E / R;
     const int nR = n / R, total = nR << lc, tmul = n / (Ns * R);
     const bool pow2 = (Ns & (Ns - 1)) == 0;
     const int lNs = 31 - __builtin_clz(Ns);
@@ -349,16 +349,16 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
 
 // runs the plan's passes in place over a C = 2^lc column tile (element i of
 // column c at buf[i*C + c]); every thread of the block must call it
-template <bool INV, int NT>
+template <bool INV, int NT, int E>
 __device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, int lc, const float2 *stw) {
     int Ns = 1;
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
-            case 4: fft_inplace_pass<4, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
-            case 2: fft_inplace_pass<2, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
-            case 3: fft_inplace_pass<3, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
-            default: fft_inplace_pass<5, INV, NT>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 4: fft_inplace_pass<4, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 2: fft_inplace_pass<2, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            case 3: fft_inplace_pass<3, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
+            default: fft_inplace_pass<5, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
         }
         Ns *= R;
     }
@@ -366,17 +366,17 @@ __device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, i
 
 // the plan's passes in place over C = 2^lc sequences with arbitrary strides
 // (row tiles: lss = n + 1, les = 1)
-template <bool INV, int NT>
+template <bool INV, int NT, int E>
 __device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl, int lc, int lss, int les,
                                                   const float2 *stw) {
     int Ns = 1;
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
-            case 4: fft_inplace_pass<4, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
-            case 2: fft_inplace_pass<2, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
-            case 3: fft_inplace_pass<3, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
-            default: fft_inplace_pass<5, INV, NT>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            case 4: fft_inplace_pass<4, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            case 2: fft_inplace_pass<2, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            case 3: fft_inplace_pass<3, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
+            default: fft_inplace_pass<5, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
         }
         Ns *= R;
     }
@@ -387,7 +387,7 @@ __device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl
 // the twiddles beside it: the row transforms of a block run together, in
 // place, instead of one 256-thread block per row with global twiddle reads.
 // grid (ceil(nb / C), B), block NT.
-template <int NT>
+template <int NT, int E>
 __global__ void __launch_bounds__(NT) k_gather_rowifft_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                              const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(NT) k_gather_rowifft_tiled(DevState st, StepAr
         tile[c * lss + (kx < 0 ? kx + np : kx)] = cmul(o, pup[row * nb + j]);            // :364
     }
     __syncthreads();
-    tile_transform_ex<true, NT>(tile, pl, lc, lss, 1, stw);                              // :365
+    tile_transform_ex<true, NT, E>(tile, pl, lc, lss, 1, stw);                              // :365
     float2 *T = st.T + ((size_t)b * nb + j0) * np;
     const float rnp = 1.0f / (float)np;
     for (int idx = threadIdx.x; idx < cs * np; idx += NT) {
@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(NT) k_gather_rowifft_tiled(DevState st, StepAr
     }
 }
 
-template <int NT>
+template <int NT, int E>
 __global__ void __launch_bounds__(NT) k_rowfft_update_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                             const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(NT) k_rowfft_update_tiled(DevState st, StepArg
     float pm = 0.f;
     for (int i = threadIdx.x; i < st.npart; i += NT) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
     pm = block_max(pm, red);  // its barriers also publish the tile
-    tile_transform_ex<false, NT>(tile, pl, lc, lss, 1, stw);                             // :394
+    tile_transform_ex<false, NT, E>(tile, pl, lc, lss, 1, stw);                             // :394
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     float2 *dP = st.dP + (size_t)b * nb * nb;
     const float rnb = 1.0f / (float)nb;
@@ -469,7 +469,7 @@ __global__ void __launch_bounds__(NT) k_rowfft_update_tiled(DevState st, StepArg
 // C: its missing columns are zero and never stored).  grid (ceil(Np / C), B),
 // block NT (256 when the tile fits its register-lifted passes, so a 16 x 200
 // tile keeps every wave busy instead of idling half of a 512-thread block).
-template <int NT>
+template <int NT, int E>
 __global__ void __launch_bounds__(NT) k_colpass_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                       const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(NT) k_colpass_tiled(DevState st, StepArgs sa, 
         if (c < cs) tile[i * C + c] = T[(size_t)j * np + x0 + c];
     }
     __syncthreads();
-    tile_transform<true, NT>(tile, pl, lc, stw);
+    tile_transform<true, NT, E>(tile, pl, lc, stw);
     // amplitude replacement, fpmMain.cpp:378-393 (same arithmetic as k_colpass)
     const float inv_n2 = 1.0f / ((float)np * (float)np);
     const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(NT) k_colpass_tiled(DevState st, StepArgs sa, 
         tile[idx] = make_float2(psi.x * sc, psi.y * sc);
     }
     __syncthreads();
-    tile_transform<false, NT>(tile, pl, lc, stw);
+    tile_transform<false, NT, E>(tile, pl, lc, stw);
     for (int idx = threadIdx.x; idx < nb * C; idx += NT) {
         const int j = idx >> lc, c = idx & cm;
         const int i = j - r < 0 ? j - r + np : j - r;
@@ -564,9 +564,9 @@ __global__ void __launch_bounds__(256) k_row_max_all(DevState st) {
 
 // ---- host-side launchers ----------------------------------------------------
 // C = 2^lc sequences of pl.n fit the in-place transform's register budget
-static bool fft_fits(const FftPlan &pl, int lc, int nt = kFftThreads) {
+static bool fft_fits(const FftPlan &pl, int lc, int nt = kFftThreads, int e = kFftRegElems) {
     for (int i = 0; i < pl.nstages; ++i)
-        if ((pl.n << lc) > fft_pass_capacity(pl.radix[i], nt)) return false;
+        if ((pl.n << lc) > fft_pass_capacity(pl.radix[i], nt, e)) return false;
     return true;
 }
 
@@ -586,8 +586,13 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     while (lr > 1 && rblk(lr) < 512) --lr;
     const size_t ldr = ((size_t)(st.np + 1) * (1 << lr) + st.np) * sizeof(float2);
     const dim3 rgrid((st.nb + (1 << lr) - 1) >> lr, st.B);
-    if (lr > 0)
-        hipLaunchKernelGGL(k_gather_rowifft_tiled<256>, rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+    // 16 register elements per thread when the tile allows (fewer VGPRs, more
+    // waves per SIMD to hide the LDS round trips of each pass), else 24
+    const bool r16 = lr > 0 && fft_fits(pl, lr, 256, 16);
+    if (lr > 0 && r16)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gather_rowifft_tiled<256, 16>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+    else if (lr > 0)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gather_rowifft_tiled<256, 24>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
     else
         hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     // tiled column pass: up to 16 columns per block while the tile fits the
@@ -601,15 +606,21 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     if (lc > 0) {
         const size_t ldt = ((size_t)st.np * (1 << lc) + st.np) * sizeof(float2);
         const dim3 grid((st.np + (1 << lc) - 1) >> lc, st.B);
-        if (fft_fits(pl, lc, 256))
-            hipLaunchKernelGGL(k_colpass_tiled<256>, grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
+        if (fft_fits(pl, lc, 256, 16))
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<256, 16>), grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
+        else if (fft_fits(pl, lc, 256))
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<256, 24>), grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
+        else if (fft_fits(pl, lc, kFftThreads, 16))
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<kFftThreads, 16>), grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
         else
-            hipLaunchKernelGGL(k_colpass_tiled<kFftThreads>, grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<kFftThreads, 24>), grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
     } else {
         hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
     }
-    if (lr > 0)
-        hipLaunchKernelGGL(k_rowfft_update_tiled<256>, rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+    if (lr > 0 && r16)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rowfft_update_tiled<256, 16>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+    else if (lr > 0)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rowfft_update_tiled<256, 24>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
     else
         hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     const int nrow = (sa.yc + st.r) / kTile - (sa.yc - st.r) / kTile + 1;
