@@ -71,6 +71,7 @@ bool make_plan(int n, FftPlan *pl) {
     std::memset(pl, 0, sizeof *pl);
     pl->n = n;
     int m = n, k = 0;
+    while (m % 8 == 0) { pl->radix[k++] = 8; m /= 8; }
     while (m % 4 == 0) { pl->radix[k++] = 4; m /= 4; }
     while (m % 2 == 0) { pl->radix[k++] = 2; m /= 2; }
     while (m % 3 == 0) { pl->radix[k++] = 3; m /= 3; }

@@ -1,4 +1,4 @@
-// fft_lds.hpp -- mixed-radix (2/3/4/5) Stockham FFT over LDS-resident
+// fft_lds.hpp -- mixed-radix (2/3/4/5/8) Stockham FFT over LDS-resident
 // sequences, plus the complex helpers shared by every FPM kernel.
 //
 // Replaces the reference's cvComplex fft2/ifft2 and cv::dft calls
@@ -57,6 +57,31 @@ __device__ __forceinline__ void dft4(float2 *v) {
     v[2] = csub(s02, s13);
     v[1] = cadd(d02, d13);
     v[3] = csub(d02, d13);
+}
+
+// radix 8 as two radix-4 DFTs (even / odd inputs) and one radix-2 stage with
+// the W8^k twiddles (k = 1, 3 cost 2 adds + 2 muls each, k = 2 is a swap)
+template <bool INV>
+__device__ __forceinline__ void dft8(float2 *v) {
+    constexpr float R2 = 0.70710678118654752440f;
+    float2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+    dft4<INV>(e);
+    dft4<INV>(o);
+    // W8 = (1 - i)/sqrt2 forward, (1 + i)/sqrt2 inverse
+    const float2 o1 = INV ? make_float2((o[1].x - o[1].y) * R2, (o[1].x + o[1].y) * R2)
+                          : make_float2((o[1].x + o[1].y) * R2, (o[1].y - o[1].x) * R2);
+    const float2 o2 = mul_mi<INV>(o[2]);
+    // W8^3 = (-1 - i)/sqrt2 forward, (-1 + i)/sqrt2 inverse
+    const float2 o3 = INV ? make_float2((-o[3].x - o[3].y) * R2, (o[3].x - o[3].y) * R2)
+                          : make_float2((o[3].y - o[3].x) * R2, (-o[3].x - o[3].y) * R2);
+    v[0] = cadd(e[0], o[0]);
+    v[4] = csub(e[0], o[0]);
+    v[1] = cadd(e[1], o1);
+    v[5] = csub(e[1], o1);
+    v[2] = cadd(e[2], o2);
+    v[6] = csub(e[2], o2);
+    v[3] = cadd(e[3], o3);
+    v[7] = csub(e[3], o3);
 }
 
 template <bool INV>
@@ -133,6 +158,7 @@ __device__ __forceinline__ void stockham_pass(const float2 *__restrict__ a, floa
         if (R == 3) dft3<INV>(v);
         if (R == 4) dft4<INV>(v);
         if (R == 5) dft5<INV>(v);
+        if (R == 8) dft8<INV>(v);
         const int base = jq * Ns * R + k;
 #pragma unroll
         for (int r = 0; r < R; ++r) dst[base + r * Ns] = v[r];
@@ -151,6 +177,7 @@ __device__ float2 *stockham(float2 *a, float2 *b, int C, const FftPlan &pl,
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
+            case 8: stockham_pass<8, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
             case 4: stockham_pass<4, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
             case 2: stockham_pass<2, INV>(a, b, n, C, Ns, tw, tid, nthr); break;
             case 3: stockham_pass<3, INV>(a, b, n, C, Ns, tw, tid, nthr); break;

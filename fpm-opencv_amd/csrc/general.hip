@@ -259,6 +259,7 @@ __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int
             if (R == 3) dft3<INV>(v[q]);
             if (R == 4) dft4<INV>(v[q]);
             if (R == 5) dft5<INV>(v[q]);
+            if (R == 8) dft8<INV>(v[q]);
             dst[q] = sq * lss + (jq * Ns * R + k) * les;
         }
     }
@@ -331,6 +332,7 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
+            case 8: fft_inplace_pass<8, INV>(smem, n, lc, lss, les, Ns, stw); break;
             case 4: fft_inplace_pass<4, INV>(smem, n, lc, lss, les, Ns, stw); break;
             case 2: fft_inplace_pass<2, INV>(smem, n, lc, lss, les, Ns, stw); break;
             case 3: fft_inplace_pass<3, INV>(smem, n, lc, lss, les, Ns, stw); break;
@@ -355,6 +357,7 @@ __device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, i
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
+            case 8: fft_inplace_pass<8, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
             case 4: fft_inplace_pass<4, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
             case 2: fft_inplace_pass<2, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
             case 3: fft_inplace_pass<3, INV, NT, E>(buf, pl.n, lc, 1, 1 << lc, Ns, stw); break;
@@ -373,6 +376,7 @@ __device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl
     for (int st = 0; st < pl.nstages; ++st) {
         const int R = pl.radix[st];
         switch (R) {
+            case 8: fft_inplace_pass<8, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
             case 4: fft_inplace_pass<4, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
             case 2: fft_inplace_pass<2, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
             case 3: fft_inplace_pass<3, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
@@ -388,7 +392,7 @@ __device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl
 // place, instead of one 256-thread block per row with global twiddle reads.
 // grid (ceil(nb / C), B), block NT.
 template <int NT, int E>
-__global__ void __launch_bounds__(NT) k_gather_rowifft_tiled(DevState st, StepArgs sa, FftPlan pl,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16 ? 4 : 1))) k_gather_rowifft_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                              const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = np + 1;
@@ -418,7 +422,7 @@ __global__ void __launch_bounds__(NT) k_gather_rowifft_tiled(DevState st, StepAr
 }
 
 template <int NT, int E>
-__global__ void __launch_bounds__(NT) k_rowfft_update_tiled(DevState st, StepArgs sa, FftPlan pl,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16 ? 4 : 1))) k_rowfft_update_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                             const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ float red[NT / 64];
@@ -470,7 +474,7 @@ __global__ void __launch_bounds__(NT) k_rowfft_update_tiled(DevState st, StepArg
 // block NT (256 when the tile fits its register-lifted passes, so a 16 x 200
 // tile keeps every wave busy instead of idling half of a 512-thread block).
 template <int NT, int E>
-__global__ void __launch_bounds__(NT) k_colpass_tiled(DevState st, StepArgs sa, FftPlan pl,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16 ? 4 : 1))) k_colpass_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                       const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, cm = C - 1;
