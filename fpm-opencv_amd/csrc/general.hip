@@ -22,6 +22,7 @@
 // forward transform are ever used.  Row passes therefore run on nb = 2r+1 rows,
 // not Np.
 #include <algorithm>
+#include <cstdlib>
 
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
@@ -515,6 +516,186 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16
     }
 }
 
+// ---- K2 (wave-private columns) ----------------------------------------------------
+// Same column pass, but every wave owns CW whole columns of the block's
+// C = NW*CW-column tile, so the radix passes synchronise the wave only (LDS
+// operations of one wave execute in issue order; the fence pair keeps the
+// compiler from moving them) instead of the whole block: two block barriers
+// per launch (after the coalesced tile load, before the coalesced store)
+// instead of two per radix pass.  Within a wave, 64/CW consecutive lanes
+// serve one column (column-major, pitch P), so a lane's column and its base
+// address are fixed for the whole transform and every butterfly element is
+// an immediate offset from it.  The measurement values a lane needs for
+// amplitude replacement (rows lane + 64q of its wave's columns) are loaded
+// into registers before the inverse transform, so their latency hides behind
+// it.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+constexpr int kWaveElems = 16;  // register elements per lane in a wave pass
+
+// one radix-R Stockham pass over the lane's column `cb` (lanes l, l + LPC,
+// ... of the column's butterflies: l = lane % LPC)
+template <int R, bool INV, int LPC>
+__device__ __forceinline__ void wave_pass(float2 *cb, int n, int Ns, const float2 *__restrict__ tw, int l) {
+    constexpr int Q = kWaveElems / R;
+    const int nR = n / R, tmul = n / (Ns * R);
+    const bool pow2 = (Ns & (Ns - 1)) == 0;
+    const int lNs = 31 - __builtin_clz(Ns);
+    const float rNs = 1.0f / (float)Ns;
+    float2 v[Q][R];
+    int base[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = l + LPC * q;
+        base[q] = -1;
+        if (j < nR) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[q][r] = cb[j + r * nR];
+            const int jq = pow2 ? (j >> lNs) : udiv(j, Ns, rNs);
+            const int k = j - jq * Ns;
+            if (Ns > 1) {
+                const int ts = tmul * k;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    float2 w = tw[r * ts];
+                    if (INV) w.y = -w.y;
+                    v[q][r] = cmul(v[q][r], w);
+                }
+            }
+            if (R == 2) dft2<INV>(v[q]);
+            if (R == 3) dft3<INV>(v[q]);
+            if (R == 4) dft4<INV>(v[q]);
+            if (R == 5) dft5<INV>(v[q]);
+            if (R == 8) dft8<INV>(v[q]);
+            base[q] = jq * Ns * R + k;
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        if (base[q] >= 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) cb[base[q] + r * Ns] = v[q][r];
+        }
+    }
+    wave_sync();
+}
+
+// The plan's radices run in reverse (smallest first: 200 = 5*5*8), so the
+// stride-R writes of the Ns = 1 pass come from a radix whose stride spreads
+// over the banks (a radix-8 first pass is a 4-way conflict on every write).
+template <bool INV, int LPC>
+__device__ __forceinline__ void wave_transform(float2 *cb, const FftPlan &pl, const float2 *stw, int l) {
+    int Ns = 1;
+    for (int s = pl.nstages - 1; s >= 0; --s) {
+        const int R = pl.radix[s];
+        switch (R) {
+            case 8: wave_pass<8, INV, LPC>(cb, pl.n, Ns, stw, l); break;
+            case 4: wave_pass<4, INV, LPC>(cb, pl.n, Ns, stw, l); break;
+            case 2: wave_pass<2, INV, LPC>(cb, pl.n, Ns, stw, l); break;
+            case 3: wave_pass<3, INV, LPC>(cb, pl.n, Ns, stw, l); break;
+            default: wave_pass<5, INV, LPC>(cb, pl.n, Ns, stw, l); break;
+        }
+        Ns *= R;
+    }
+}
+
+// column pitch of the tile: Np rounded to 2 mod 4, so the C columns of the
+// coalesced load/store land in distinct banks and every column is 16-byte
+// aligned
+int colw_pitch(int np) {
+    int p = np;
+    while ((p & 3) != 2) ++p;
+    return p;
+}
+
+// grid (ceil(Np / (NW*CW)), B), block 64*NW, LDS (NW*CW*pitch + Np) float2
+template <int NW, int CW>
+__global__ void __launch_bounds__(64 * NW)
+k_colpass_wave(DevState st, StepArgs sa, FftPlan pl, const float2 *__restrict__ tw, int P) {
+    constexpr int NT = 64 * NW, C = NW * CW, NQY = 16 / CW;
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const int np = st.np, r = st.r, nb = st.nb;
+    const int x0 = blockIdx.x * C, b = blockIdx.y;
+    const int cs = min(C, np - x0);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int LPC = 64 / CW;
+    float2 *stw = smem + (size_t)C * P;
+    float2 *wb = smem + (size_t)w * CW * P;
+    float2 *cb = wb + (lane / LPC) * P;  // this lane's column in the radix passes
+    const int l = lane % LPC;
+    float2 *T = st.T + (size_t)b * nb * np;
+    // this lane's measurement values: rows lane + 64q of the wave's columns
+    const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
+    uint16_t iv[NQY * CW];
+#pragma unroll
+    for (int q = 0; q < NQY; ++q) {
+        const int y = lane + 64 * q;
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const int x = w * CW + c;
+            iv[q * CW + c] = (y < np && x < cs) ? I[(size_t)y * np + x0 + x] : (uint16_t)0;
+        }
+    }
+    for (int i = threadIdx.x; i < np; i += NT) stw[i] = tw[i];
+    // every tile element written once: box rows from T, zeros elsewhere
+    const float rC = 1.0f / (float)C;
+    for (int idx = threadIdx.x; idx < np * C; idx += NT) {
+        const int i = udiv(idx, C, rC), c = idx - i * C;
+        const int ky = i < np / 2 ? i : i - np, j = ky + r;
+        float2 v = make_float2(0.f, 0.f);
+        if (c < cs && j >= 0 && j < nb) v = T[(size_t)j * np + x0 + c];
+        smem[c * P + i] = v;
+    }
+    __syncthreads();
+    wave_transform<true, LPC>(cb, pl, stw, l);
+    // amplitude replacement, fpmMain.cpp:378-393 (same arithmetic as k_colpass)
+    const float inv_n2 = 1.0f / ((float)np * (float)np);
+#pragma unroll
+    for (int q = 0; q < NQY; ++q) {
+        const int y = lane + 64 * q;
+        if (y >= np) continue;
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            float2 *e = wb + c * P + y;
+            const float2 psi = cscale(*e, inv_n2);
+            const float a = sqrtf((float)iv[q * CW + c]);
+            const float tre = psi.x + st.eps;
+            const float mag = sqrtf(tre * tre + psi.y * psi.y);
+            const float sc = a / mag;
+            *e = make_float2(psi.x * sc, psi.y * sc);
+        }
+    }
+    wave_sync();
+    wave_transform<false, LPC>(cb, pl, stw, l);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nb * C; idx += NT) {
+        const int j = udiv(idx, C, rC), c = idx - j * C;
+        const int i = j - r < 0 ? j - r + np : j - r;
+        if (c < cs) T[(size_t)j * np + x0 + c] = smem[c * P + i];
+    }
+}
+
+// columns per wave of k_colpass_wave for this plan: the largest CW in {4,2,1}
+// for which 64/CW lanes hold a column's butterflies in every radix pass
+// (kWaveElems values per lane);
+// 0 when even one column does not fit
+int colw_cw(const FftPlan &pl) {
+    for (int cw = 4; cw >= 1; cw >>= 1) {
+        bool ok = true;
+        for (int i = 0; i < pl.nstages; ++i) {
+            const int R = pl.radix[i];
+            const int lpc = 64 / cw;
+            if ((pl.n / R + lpc - 1) / lpc > kWaveElems / R) ok = false;
+        }
+        if (ok) return cw;
+    }
+    return 0;
+}
+
 // sqrt of the init image as complex, fpmMain.cpp:319-322. grid (Np, B)
 __global__ void k_init_amp(const uint16_t *__restrict__ meas, float2 *__restrict__ out, int np, int B,
                            int led, size_t out_bs) {
@@ -607,7 +788,21 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     while (lc > 0 && !fft_fits(pl, lc)) --lc;
     auto nblk = [&](int l) { return ((st.np + (1 << l) - 1) >> l) * st.B; };
     while (lc > 2 && nblk(lc) < 512) --lc;
-    if (lc > 0) {
+    const int cw = colw_cw(pl);
+    if (cw > 1 && !std::getenv("FPM_NO_WAVE_COLS")) {
+        // wave-private columns: 4 waves x CW columns, 8 waves when a wave
+        // holds a single (long) column
+        const int P = colw_pitch(st.np);
+        const int nw = cw == 1 ? 8 : 4, C = nw * cw;
+        const size_t ldw = ((size_t)C * P + st.np) * sizeof(float2);
+        const dim3 grid((st.np + C - 1) / C, st.B);
+        if (cw == 4)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<4, 4>), grid, dim3(256), ldw, s, st, sa, pl, tw, P);
+        else if (cw == 2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<4, 2>), grid, dim3(256), ldw, s, st, sa, pl, tw, P);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<8, 1>), grid, dim3(512), ldw, s, st, sa, pl, tw, P);
+    } else if (lc > 0) {
         const size_t ldt = ((size_t)st.np * (1 << lc) + st.np) * sizeof(float2);
         const dim3 grid((st.np + (1 << lc) - 1) >> lc, st.B);
         if (fft_fits(pl, lc, 256, 16))
