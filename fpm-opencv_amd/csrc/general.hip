@@ -373,8 +373,10 @@ __device__ __forceinline__ void tile_transform(float2 *buf, const FftPlan &pl, i
 template <bool INV, int NT, int E>
 __device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl, int lc, int lss, int les,
                                                   const float2 *stw) {
+    // radices smallest first, as in wave_transform: the stride-R writes of
+    // the Ns = 1 pass then spread over the banks
     int Ns = 1;
-    for (int st = 0; st < pl.nstages; ++st) {
+    for (int st = pl.nstages - 1; st >= 0; --st) {
         const int R = pl.radix[st];
         switch (R) {
             case 8: fft_inplace_pass<8, INV, NT, E>(buf, pl.n, lc, lss, les, Ns, stw); break;
@@ -388,6 +390,16 @@ __device__ __forceinline__ void tile_transform_ex(float2 *buf, const FftPlan &pl
 }
 
 // ---- K1 / K3 (tiled) ------------------------------------------------------------
+// Row pitch of a C = 2^lc row tile: >= Np + 1 and = 32/C (mod 32), so the C
+// rows a 32-lane read group touches (32/C consecutive elements each) are
+// 64/C banks apart and cover the 64 banks once (Np + 1 put the C rows 2 banks
+// apart: 2-4 way conflicts on every pass read).
+__host__ __device__ inline int row_pitch(int np, int lc) {
+    const int m = lc >= 5 ? 1 : 32 >> lc;
+    int p = np + 1;
+    while ((p & 31) != (m & 31)) ++p;
+    return p;
+}
 // C = 2^lc box rows per block in one row-major LDS tile (pitch Np + 1) with
 // the twiddles beside it: the row transforms of a block run together, in
 // place, instead of one 256-thread block per row with global twiddle reads.
@@ -396,7 +408,7 @@ template <int NT, int E>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16 ? 4 : 1))) k_gather_rowifft_tiled(DevState st, StepArgs sa, FftPlan pl,
                                                              const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = np + 1;
+    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = row_pitch(np, lc);
     const int j0 = blockIdx.x << lc, b = blockIdx.y;
     const int cs = min(C, nb - j0);
     float2 *tile = smem, *stw = smem + (size_t)C * lss;
@@ -427,7 +439,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16
                                                             const float2 *__restrict__ tw, int lc) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ float red[NT / 64];
-    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = np + 1;
+    const int np = st.np, r = st.r, nb = st.nb, C = 1 << lc, lss = row_pitch(np, lc);
     const int j0 = blockIdx.x << lc, b = blockIdx.y;
     const int cs = min(C, nb - j0);
     float2 *tile = smem, *stw = smem + (size_t)C * lss;
@@ -769,7 +781,7 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     while (lr > 0 && !fft_fits(pl, lr, 256)) --lr;
     auto rblk = [&](int l) { return ((st.nb + (1 << l) - 1) >> l) * st.B; };
     while (lr > 1 && rblk(lr) < 512) --lr;
-    const size_t ldr = ((size_t)(st.np + 1) * (1 << lr) + st.np) * sizeof(float2);
+    const size_t ldr = ((size_t)row_pitch(st.np, lr) * (1 << lr) + st.np) * sizeof(float2);
     const dim3 rgrid((st.nb + (1 << lr) - 1) >> lr, st.B);
     // 16 register elements per thread when the tile allows (fewer VGPRs, more
     // waves per SIMD to hide the LDS round trips of each pass), else 24
