@@ -193,3 +193,24 @@ def test_fused_more_patches_than_cus():
         ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, 10, 3, 1)
         assert rel_l2(out["objCrop"][b], ref["objCrop"]) < 1e-5
         assert rel_l2(out["pupil"][b], ref["pupil"]) < 1e-5
+
+
+@pytest.mark.parametrize("Np,L,r", [(200, 600, 26), (90, 360, 30), (64, 192, 10)])
+def test_wave_and_tiled_column_passes_agree(Np, L, r, monkeypatch):
+    """The wave-private column pass (k_colpass_wave, the default wherever a
+    wave holds >= 2 columns) and the block-tiled one (k_colpass_tiled,
+    FPM_NO_WAVE_COLS=1) compute the same transforms with different pass
+    orders: both match the oracle and each other far inside the tolerance."""
+    x0, y0, order = grid_geometry(Np, L, 3, max(1, r // 3))
+    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=11)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2, path=fpm_amd.PATH_GENERAL)
+    wave = fpm_amd.run_fpm(prob, stack, 2)
+    monkeypatch.setenv("FPM_NO_WAVE_COLS", "1")
+    tiled = fpm_amd.run_fpm(prob, stack, 2)
+    ref = oracle_run(stack[:, 1], order, x0, y0, Np, L, r, 5, 10, 2)
+    for out in (wave, tiled):
+        assert rel_l2(out["objCrop"][1], ref["objCrop"]) < _tol(2)
+        assert rel_l2(out["pupil"][1], ref["pupil"]) < _tol(2)
+    for b in range(2):
+        assert rel_l2(wave["objCrop"][b], tiled["objCrop"][b]) < 2e-6
+        assert rel_l2(wave["pupil"][b], tiled["pupil"][b]) < 2e-6
