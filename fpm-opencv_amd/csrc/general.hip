@@ -137,10 +137,13 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
 }
 
 // ---- K4 ---------------------------------------------------------------------
-// grid (ROI tile rows, B), block 256: one tile row of the ROI box per block.
+// grid (ROI tile rows, B), block 256 or 1024: one tile row of the ROI box per block.
 // Each wave refreshes whole 16x16 tiles (4 pixels per lane, no barrier); the
 // block then folds the row's other (unchanged) tile maxima into rmax.
-constexpr int kRowThreads = 1024;
+// Block size: one wave per ROI tile column up to 16 waves (1024 threads for
+// config 5's 42-tile rows; 256 for config 3's 4-5 tiles, where 16 mostly
+// idle waves per block only added latency).
+template <int kRowThreads>
 __global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs sa) {
     __shared__ float red[kRowThreads / 64];
     extern __shared__ float fresh[];  // the ROI's tiles of this row
@@ -178,33 +181,44 @@ __global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs
 // row maxima, then P += num / max * S (fpmMain.cpp:470-475) on this block's
 // slice of the support box and its partial max|P| for the next LED (:415).
 constexpr int kCommitThreads = 256;
+constexpr int kCommitPx = 1024;  // support-box pixels per K5 block (a multiple of kCommitThreads)
 __global__ void __launch_bounds__(kCommitThreads) k_pupil_commit(DevState st) {
     __shared__ float red[kCommitThreads / 64];
     const int nb = st.nb, b = blockIdx.y, part = blockIdx.x;
     const float *rmax = st.rmax + (size_t)b * st.nty;
-    float m = 0.f;
-    for (int i = threadIdx.x; i < st.nty; i += kCommitThreads) m = fmaxf(m, rmax[i]);
-    const float omax = block_max(m, red);
     const int n = nb * nb, chunk = (n + st.npart - 1) / st.npart;
     const int i0 = part * chunk, i1 = min(n, i0 + chunk);
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     const float2 *dP = st.dP + (size_t)b * nb * nb;
+    // this thread's pixels (chunk <= kCommitPx) are loaded before the max
+    // reduction, so their latency overlaps the rmax round trip
+    constexpr int KP = kCommitPx / kCommitThreads;
+    float2 pv[KP], dv[KP];
+    bool on[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const int i = i0 + threadIdx.x + k * kCommitThreads;
+        on[k] = i < i1 && st.disk[i];
+        pv[k] = on[k] ? pup[i] : make_float2(0.f, 0.f);
+        dv[k] = on[k] ? dP[i] : make_float2(0.f, 0.f);
+    }
+    float m = 0.f;
+    for (int i = threadIdx.x; i < st.nty; i += kCommitThreads) m = fmaxf(m, rmax[i]);
+    const float omax = block_max(m, red);
     float pm = 0.f;
-    for (int i = i0 + threadIdx.x; i < i1; i += kCommitThreads) {
-        if (!st.disk[i]) continue;
-        float2 p = pup[i];
-        const float2 d = dP[i];
-        p.x += d.x / omax;
-        p.y += d.y / omax;
-        pup[i] = p;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        if (!on[k]) continue;
+        float2 p = pv[k];
+        p.x += dv[k].x / omax;
+        p.y += dv[k].y / omax;
+        pup[i0 + threadIdx.x + k * kCommitThreads] = p;
         pm = fmaxf(pm, cmag(p));
     }
     pm = block_max(pm, red);
     if (threadIdx.x == 0) st.pmax[b * st.npart + part] = pm;
 }
 
-// support-box pixels per K5 block
-constexpr int kCommitPx = 1024;
 int pupil_parts(int nb) { return std::max(1, (nb * nb + kCommitPx - 1) / kCommitPx); }
 
 // ---- init / output kernels -------------------------------------------------
@@ -836,7 +850,10 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
         hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     const int nrow = (sa.yc + st.r) / kTile - (sa.yc - st.r) / kTile + 1;
     const int ncol = (sa.xc + st.r) / kTile - (sa.xc - st.r) / kTile + 1;
-    hipLaunchKernelGGL(k_tile_rows, dim3(nrow, st.B), dim3(kRowThreads), ncol * sizeof(float), s, st, sa);
+    if (ncol > 8)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<1024>), dim3(nrow, st.B), dim3(1024), ncol * sizeof(float), s, st, sa);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<256>), dim3(nrow, st.B), dim3(256), ncol * sizeof(float), s, st, sa);
     hipLaunchKernelGGL(k_pupil_commit, dim3(st.npart, st.B), dim3(kCommitThreads), 0, s, st);
     return hipGetLastError();
 }
