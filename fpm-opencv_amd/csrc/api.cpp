@@ -254,6 +254,21 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     st.eps = (float)prob->eps;
     make_plan(np, &c->pl_np);
     make_plan(L, &c->pl_L);
+    // live band of the centred spectrum (fpm_state.hpp): the init placement at
+    // L/2 (fpmMain.cpp:332-343) and every used LED's support box (:405-447)
+    st.sy0 = st.sx0 = L / 2 - r;
+    st.sy1 = st.sx1 = L / 2 + r;
+    for (int i = 0; i < prob->n_order; ++i) {
+        const int led = c->order[i];
+        st.sy0 = std::min(st.sy0, c->y0[led] + np / 2 - r);
+        st.sy1 = std::max(st.sy1, c->y0[led] + np / 2 + r);
+        st.sx0 = std::min(st.sx0, c->x0[led] + np / 2 - r);
+        st.sx1 = std::max(st.sx1, c->x0[led] + np / 2 + r);
+    }
+    st.sy0 = std::max(st.sy0, 0);
+    st.sx0 = std::max(st.sx0, 0);
+    st.sy1 = std::min(st.sy1, L - 1);
+    st.sx1 = std::min(st.sx1, L - 1);
 
     // support disk on the box: Euclidean disk == filled cv::circle (fpmMain.cpp:307)
     std::vector<uint8_t> disk((size_t)nb * nb);

@@ -53,6 +53,11 @@ struct DevState {
     int npart;        // partial max|P| values per patch
     float delta1, delta2, eps;
     float hscale, hinv;  // fp16 storage scale and its inverse (powers of two)
+    // live band of the centred spectrum, inclusive: spec is zeroed by fpm_init
+    // and only ever changes on the support boxes of the init placement
+    // (L/2 +- r) and of the used LEDs ((crop0 + Np/2) +- r), so rows outside
+    // [sy0, sy1] and columns outside [sx0, sx1] stay exactly 0 (objCrop skips them)
+    int sy0, sy1, sx0, sx1;
 };
 
 // spectrum element i of patch b (i = y*L + x in the centred spectrum)

@@ -24,6 +24,13 @@
 #include "dft16.hpp"
 #include "fpm_state.hpp"
 
+#ifndef FPM_CROP_UNROLL
+#define FPM_CROP_UNROLL 4   // strip load/store loop unroll (loads in flight per thread)
+#endif
+#define FPM_CROP_STR_(x) #x
+#define FPM_CROP_STR(x) FPM_CROP_STR_(x)
+#define FPM_CROP_PRAGMA_UNROLL _Pragma(FPM_CROP_STR(unroll FPM_CROP_UNROLL))
+
 namespace fpm {
 
 namespace {
@@ -85,10 +92,18 @@ __device__ __forceinline__ void load_twiddles(float2 *twL, const float2 *__restr
     for (int m = 0; m < 16; ++m) wt[m] = twL[((m * t) & 255) * step];  // W256^{mt} = W_L^{M m t}
 }
 
-// pass 1: row IDFTs of fftShift(spec).  grid (L / G, B), block 16 G
+// live-band test: a <= i <= b
+__device__ __forceinline__ bool in_band(int i, int a, int b) { return (unsigned)(i - a) <= (unsigned)(b - a); }
+
+// pass 1: row IDFTs of fftShift(spec) over the live rows [sy0, sy1] only
+// (fpm_state.hpp: every other spec row is exactly zero, so its objF row's
+// IDFT is zero; pass 2 treats those rows as zero instead of reading them),
+// loading only the live columns [sx0, sx1].  grid (ceil((sy1-sy0+1) / G), B),
+// block 16 G
 template <int M, int G>
 __global__ void __launch_bounds__(16 * G) k_crop_rows(const float2 *__restrict__ spec, float2 *__restrict__ out,
-                                                      const float2 *__restrict__ tw_L) {
+                                                      const float2 *__restrict__ tw_L, int sy0, int sy1, int sx0,
+                                                      int sx1) {
     constexpr int L = 256 * M;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2 *twL = sm;                  // L
@@ -98,15 +113,20 @@ __global__ void __launch_bounds__(16 * G) k_crop_rows(const float2 *__restrict__
     float2 *scr = scr_all + g * XTILE;
     float2 wt[16];
     load_twiddles(twL, tw_L, L, M, wt, t);
-    const int b = blockIdx.y, row = blockIdx.x * G + g;
-    const int srow = row + L / 2 < L ? row + L / 2 : row - L / 2;       // objF row = spec row + L/2
-    const float2 *src = spec + (size_t)b * L * L + (size_t)srow * L;
+    const int b = blockIdx.y, srow = sy0 + blockIdx.x * G + g;
+    const bool live = srow <= sy1;     // group-uniform; no block barrier follows
+    const int row = srow + L / 2 < L ? srow + L / 2 : srow - L / 2;     // objF row = spec row + L/2
+    const float2 *src = spec + (size_t)b * L * L + (size_t)(live ? srow : sy1) * L;
     float2 x[M][16];
 #pragma unroll
     for (int j = 0; j < 16; ++j)
 #pragma unroll
-        for (int c = 0; c < M; ++c) x[c][(j + 8) & 15] = src[M * (t + 16 * j) + c];  // element roll by L/2
+        for (int c = 0; c < M; ++c) {  // element roll by L/2
+            const int sc = M * (t + 16 * j) + c;
+            x[c][(j + 8) & 15] = in_band(sc, sx0, sx1) ? src[sc] : make_float2(0.f, 0.f);
+        }
     dftL_regs<M, true>(x, scr, wt, twL, t, xrd);
+    if (!live) return;
     float2 *dst = out + (size_t)b * L * L + (size_t)row * L;
 #pragma unroll
     for (int p = 0; p < M; ++p)
@@ -120,9 +140,11 @@ __global__ void __launch_bounds__(16 * G) k_crop_rows(const float2 *__restrict__
 // the compile-time set r + 16 p < 8 M on output (k = t + 16 r + 256 p), so a
 // half-size strip (58 KB at L = 768) lets two blocks share a CU and overlap
 // one block's HBM phase with the other's transform.
+// Rows of the intermediate outside the live band (objF row i <-> spec row
+// i + L/2 mod L) were not written by pass 1 and are read as zero.
 template <int M, int G>
 __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
-                                                      float scale) {
+                                                      float scale, int sy0, int sy1) {
     constexpr int L = 256 * M, H = L / 2;
     constexpr int SP = G + 1;          // strip row pitch (complex)
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
@@ -141,9 +163,12 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
     float2 x[M][16];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+        // objF row y + h H is spec row y + (1 - h) H: the live rows of this
+        // half are the contiguous range [ya, yb]
+        const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
         // strip load: consecutive threads take consecutive columns of a row
-#pragma unroll 4
-        for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
+FPM_CROP_PRAGMA_UNROLL
+        for (int idx = ya * G + threadIdx.x; idx < (yb + 1) * G; idx += NTH) {
             const int y = idx / G, cc = idx - y * G;
             strip[y * SP + cc] = base[(size_t)(y + h * H) * L + cc];
         }
@@ -151,7 +176,10 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
 #pragma unroll
         for (int j = 8 * h; j < 8 * h + 8; ++j)
 #pragma unroll
-            for (int c = 0; c < M; ++c) x[c][j] = strip[(M * (t + 16 * j) + c - h * H) * SP + g];
+            for (int c = 0; c < M; ++c) {
+                const int y = M * (t + 16 * j) + c - h * H;
+                x[c][j] = (y >= ya && y <= yb) ? strip[y * SP + g] : make_float2(0.f, 0.f);  // ya > yb: none
+            }
         __syncthreads();
     }
     dftL_regs<M, true>(x, scr, wt, twL, t, xrd);
@@ -165,7 +193,7 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
                 if ((r + 16 * p < 8 * M) == (h == 0))
                     strip[(t + 16 * r + 256 * p - h * H) * SP + g] = cscale(x[p][r], scale);
         __syncthreads();
-#pragma unroll 4
+FPM_CROP_PRAGMA_UNROLL
         for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
             const int y = idx / G, cc = idx - y * G;
             base[(size_t)(y + h * H) * L + cc] = strip[y * SP + cc];
@@ -186,10 +214,13 @@ hipError_t launch_crop(const DevState &st, float2 *out, const float2 *tw_L, hipS
     e = hipFuncSetAttribute((const void *)k_crop_cols<M, G>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_cols);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_crop_rows<M, GR>), dim3(L / GR, st.B), dim3(16 * GR), lds_rows, s,
-                       (const float2 *)st.spec, out, tw_L);
+    if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1)
+        return hipErrorInvalidValue;
+    const int nrows = st.sy1 - st.sy0 + 1;
+    hipLaunchKernelGGL((k_crop_rows<M, GR>), dim3((nrows + GR - 1) / GR, st.B), dim3(16 * GR), lds_rows, s,
+                       (const float2 *)st.spec, out, tw_L, st.sy0, st.sy1, st.sx0, st.sx1);
     hipLaunchKernelGGL((k_crop_cols<M, G>), dim3(L / G, st.B), dim3(16 * G), lds_cols, s, out, tw_L,
-                       1.0f / ((float)L * (float)L));
+                       1.0f / ((float)L * (float)L), st.sy0, st.sy1);
     return hipGetLastError();
 }
 
