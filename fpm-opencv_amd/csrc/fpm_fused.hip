@@ -67,6 +67,10 @@ struct FusedArgs {
     // tail row q holds pixels tail_px[p0 .. p0+np) with kx = kx0, kx0+1, ...
     int tail_row_p0[fz::MAXTAILROWS], tail_row_np[fz::MAXTAILROWS], tail_row_kx0[fz::MAXTAILROWS];
     int ntiles, nwords;         // tiles of |spec| maxima, 32-bit words of the dirty bitmap
+    // tiles of the spectrum's live band (fpm_state.hpp): every other tile is
+    // exactly 0 and never dirty, so max|objF| only scans these nbt tiles
+    int btx0, bty0, nbx, nbt;
+    float rnbx;                 // 1 / nbx
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
 };
 
@@ -559,8 +563,16 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 
         // ---- exact max|objF| (:460,467): max over clean tiles; dirty tiles
         // only matter (and are re-read) when their bound exceeds that max
+        // band tile k -> tile (ty, tx); (k + 0.5) / nbx is never within float
+        // rounding of an integer for k < 2^16
+        auto band_ty = [&](int k) { return a.bty0 + (int)(((float)k + 0.5f) * a.rnbx); };
+        auto band_tile = [&](int k) {
+            const int dy = (int)(((float)k + 0.5f) * a.rnbx);
+            return (a.bty0 + dy) * st.ntx + a.btx0 + (k - dy * a.nbx);
+        };
         float cm = 0.f, dm = 0.f;
-        for (int i = tid; i < a.ntiles; i += NT) {
+        for (int k = tid; k < a.nbt; k += NT) {
+            const int i = band_tile(k);
             const bool d = (dirty[i >> 5] >> (i & 31)) & 1u;
             if (d) dm = fmaxf(dm, tmx[i]);
             else cm = fmaxf(cm, tmx[i]);
@@ -581,9 +593,10 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         }
         float omax = cm;
         if (dm > cm) {  // block-uniform: rare (bright-field LEDs, first LED of an iteration)
-            for (int i = w; i < a.ntiles; i += NT / 64) {
+            for (int k = w; k < a.nbt; k += NT / 64) {
+                const int i = band_tile(k);
                 if (!((dirty[i >> 5] >> (i & 31)) & 1u) || !(tmx[i] > cm)) continue;  // wave-uniform
-                const int ty = i / st.ntx, tx = i - ty * st.ntx;
+                const int ty = band_ty(k), tx = i - ty * st.ntx;
                 float mm = 0.f;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
@@ -598,8 +611,10 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             }
             __syncthreads();
             float m2 = 0.f;
-            for (int i = tid; i < a.ntiles; i += NT)
+            for (int k = tid; k < a.nbt; k += NT) {
+                const int i = band_tile(k);
                 if (!((dirty[i >> 5] >> (i & 31)) & 1u)) m2 = fmaxf(m2, tmx[i]);
+            }
             m2 = wave_max(m2);
             __syncthreads();  // red[] reads above are done
             if (lane == 0) red[w] = m2;
@@ -772,6 +787,13 @@ hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, co
     for (int i = 0; i < fz::MAXTAIL; ++i) a.tail_px[i] = i < g.n_tail_px ? g.tail_px[i] : make_int2(0, 0);
     a.ntiles = st.ntx * st.nty;
     a.nwords = (a.ntiles + 31) / 32;
+    if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
+        return hipErrorInvalidValue;
+    a.bty0 = st.sy0 / kTile;
+    a.btx0 = st.sx0 / kTile;
+    a.nbx = st.sx1 / kTile - a.btx0 + 1;
+    a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
+    a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
     const size_t lds = fused_lds_bytes(a.ntiles, g.n_tail_rows);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_iteration, hipFuncAttributeMaxDynamicSharedMemorySize,
