@@ -389,16 +389,21 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 // twiddle index advances by x per term
                 const int q = idx / TH, xl = idx - q * TH, x = xl + TH * h;
                 const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
-                int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
+                // twiddle W^{-x kx} by recurrence from two table values: a
+                // per-term table read with lane-dependent x conflicts on LDS banks
+                // (even and odd terms on two chains)
+                const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
+                float2 wa = cconj(tw[ti]), wb = cconj(tw[(ti + x) & (NP - 1)]);
+                const float2 wstep = cconj(tw[(2 * x) & (NP - 1)]);
                 float2 s2 = make_float2(0.f, 0.f), s3 = make_float2(0.f, 0.f);
                 int p = 0;
                 for (; p + 1 < np_; p += 2) {
-                    const int tj = (ti + x) & (NP - 1);
-                    s2 = cadd(s2, cmul(tailX[p0 + p], cconj(tw[ti])));
-                    s3 = cadd(s3, cmul(tailX[p0 + p + 1], cconj(tw[tj])));
-                    ti = (tj + x) & (NP - 1);
+                    s2 = cadd(s2, cmul(tailX[p0 + p], wa));
+                    s3 = cadd(s3, cmul(tailX[p0 + p + 1], wb));
+                    wa = cmul(wa, wstep);
+                    wb = cmul(wb, wstep);
                 }
-                if (p < np_) s2 = cadd(s2, cmul(tailX[p0 + p], cconj(tw[ti])));
+                if (p < np_) s2 = cadd(s2, cmul(tailX[p0 + p], wa));
                 th[(NROWS + q) * TLD + xl] = cadd(s2, s3);
             }
             __syncthreads();  // half-T complete
@@ -489,11 +494,15 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             for (int pp = g; pp < a.n_tail_px; pp += NG) {  // tail pixels: 16 lanes sum 128 terms
                 const int2 px = tpx[pp];
                 const float2 *row = th + sig[px.x + KYOFF] * TLD;
+                // W^{x kx} for x = t + 16 m + TH h by recurrence over m (two
+                // table reads instead of eight bank-conflicting ones)
                 float2 s2 = make_float2(0.f, 0.f);
+                float2 wk = tw[((t + TH * h) * (px.y + NP)) & (NP - 1)];
+                const float2 wstep = tw[(16 * (px.y + NP)) & (NP - 1)];
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {
-                    const int xl = t + 16 * m;
-                    s2 = cadd(s2, cmul(row[xl], tw[((xl + TH * h) * (px.y + NP)) & (NP - 1)]));
+                    s2 = cadd(s2, cmul(row[t + 16 * m], wk));
+                    if (m < 7) wk = cmul(wk, wstep);
                 }
 #pragma unroll
                 for (int o = 8; o > 0; o >>= 1) {
