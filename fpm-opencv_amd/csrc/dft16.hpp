@@ -82,7 +82,17 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], float2 (&r)[16]) {
 // once per kernel: every read may alias every write and stays after them,
 // while unrelated loads and stores remain free to move across the exchange
 // (a wave_barrier/fence pair here pinned them and cost 7% of the kernel).
-constexpr int XP = 17;                      // exchange-tile row pitch
+//
+// With an even pitch (18 complex = 144 B, every row 16-B aligned) each lane
+// reads its row as eight ds_read_b128 instead of sixteen 8-byte reads (which
+// the compiler pairs into ds_read2_b64, half the LDS bytes per clock). Banks:
+// row t starts at dword 36 t = 4 (9 t mod 16) (mod 64), a distinct 16-byte
+// slot for each t, and every ds_read_b128 lane group holds 16 distinct t, so
+// the wide reads are conflict-free; the 16-lane row writes stay contiguous.
+#ifndef FPM_XP
+#define FPM_XP 18
+#endif
+constexpr int XP = FPM_XP;                  // exchange-tile row pitch
 constexpr int XTILE = 16 * XP;              // complex per group tile
 __device__ __forceinline__ int opaque_int(int v) {
     asm volatile("" : "+v"(v));
@@ -96,8 +106,18 @@ __device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const fl
     (void)t;
 #pragma unroll
     for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
+    if constexpr (XP % 2 == 0) {
+        const float4 *rp = (const float4 *)(scr + xrd);  // 16-B aligned: XTILE and XP even
 #pragma unroll
-    for (int j = 0; j < 16; ++j) z[j] = scr[xrd + j];
+        for (int j = 0; j < 8; ++j) {
+            const float4 q = rp[j];
+            z[2 * j] = make_float2(q.x, q.y);
+            z[2 * j + 1] = make_float2(q.z, q.w);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) z[j] = scr[xrd + j];
+    }
 }
 
 }  // namespace fpm
