@@ -520,10 +520,15 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         // tile max (LDS atomic max on the float bits); a tile whose maximum
         // pixel decreased is marked dirty (its value becomes an upper bound).
         unsigned *tmu = (unsigned *)tmx;
+        // The atomic max is issued only when the new value exceeds the tile
+        // maximum this lane read: tmu only grows, so a skipped max was never
+        // needed (64 lanes of a wave hit 2-4 tile words, and an unfiltered
+        // LDS atomic serialises them: 3.7k cycles per LED).
         auto note = [&](int py, int px, float ao, float an) {
             const int ti = (py >> 4) * st.ntx + (px >> 4);
-            if (an < ao && tmu[ti] <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
-            atomicMax(&tmu[ti], __float_as_uint(an));
+            const unsigned cur = tmu[ti];
+            if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
+            if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
         // Straight-line over all slots: outside the support O = P = 0, so the
         // numerator is exactly 0 and only the spectrum store and the tile
