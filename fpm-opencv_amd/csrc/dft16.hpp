@@ -69,10 +69,11 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], float2 (&r)[16]) {
 
 // ------------------------------------------------------- four-step exchange
 // Lane t of a 16-lane group holds y[m1] (m1 = 0..15); afterwards lane t holds
-// z[j] = y_of_lane_j[t].  The 16x16 tile has a row pitch of 17 complex: the
-// write (16 lanes, one row) and the read (32 lanes = two groups 2176 B apart)
-// are bank-conflict free, and every access is one base register plus an
-// immediate offset (an XOR swizzle would need 32 per-lane address registers).
+// z[j] = y_of_lane_j[t].  The 16x16 tile is padded (row pitch XP complex):
+// the write (16 lanes, one row) and the read are bank-conflict free, and every
+// access is one base register plus an immediate offset (an XOR swizzle would
+// need 32 per-lane address registers).  Pitch 17 (odd) suits 8-byte reads;
+// pitch 18 (below) allows 16-byte reads.
 //
 // Ordering: LDS instructions of one wave execute in issue order, so the reads
 // see every lane's writes as long as the COMPILER keeps them in program

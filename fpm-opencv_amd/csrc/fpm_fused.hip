@@ -23,8 +23,8 @@
 //
 // 256-point transforms are 16x16 four-step DFTs: a 16-lane group holds 16
 // complex values per lane (element index = lane + 16*register), does the two
-// 16-point DFTs in registers and exchanges once through a padded (pitch 17),
-// conflict-free LDS tile.  The row IDFT input, the row DFT output and the
+// 16-point DFTs in registers and exchanges once through a padded (pitch 18),
+// conflict-free LDS tile (dft16.hpp).  The row IDFT input, the row DFT output and the
 // pupil/object registers share the "kx = lane + 16*k" layout, so P and the
 // pre-update O never move.  Only k in {0,1,2,13,14,15} (|kx| <= 47) can be
 // inside the support, so inputs of the inverse transforms and outputs of the
