@@ -214,3 +214,29 @@ def test_wave_and_tiled_column_passes_agree(Np, L, r, monkeypatch):
     for b in range(2):
         assert rel_l2(wave["objCrop"][b], tiled["objCrop"][b]) < 2e-6
         assert rel_l2(wave["pupil"][b], tiled["pupil"][b]) < 2e-6
+
+
+@pytest.mark.parametrize("L,step", [(512, 60), (768, 100), (1024, 150)])
+def test_objcrop_live_band(L, step):
+    """objCrop transforms only the live band of the spectrum (rows/columns the
+    init placement and the used LEDs' support boxes reach, fpm_state.hpp):
+    with an LED set off to one side the band is asymmetric, the spectrum is
+    exactly zero outside it, and objCrop still equals the dense IDFT of objF
+    (numpy, complex128) computed from the GPU's own spectrum."""
+    Np, r = 256, 33
+    c = L // 2 - Np // 2
+    x0 = np.array([c, c + step, c + 2 * step, c + step])
+    y0 = np.array([c, c, c - step, c - 2 * step])
+    order = [0, 1, 2, 3]
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=41)
+    out = fpm_amd.run_fpm(fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3), stack, 1)
+    spec = np.fft.fftshift(out["objF"][0])
+    sy0, sy1 = min(L // 2 - r, y0.min() + Np // 2 - r), max(L // 2 + r, y0.max() + Np // 2 + r)
+    sx0, sx1 = min(L // 2 - r, x0.min() + Np // 2 - r), max(L // 2 + r, x0.max() + Np // 2 + r)
+    assert sy1 - sy0 + 1 < L and sx1 - sx0 + 1 < L
+    live = np.zeros((L, L), bool)
+    live[sy0:sy1 + 1, sx0:sx1 + 1] = True
+    assert np.count_nonzero(spec[~live]) == 0
+    assert np.count_nonzero(spec[live]) > 0
+    ref = np.fft.ifft2(out["objF"][0].astype(np.complex128))
+    assert rel_l2(out["objCrop"][0], ref) < 2e-6
