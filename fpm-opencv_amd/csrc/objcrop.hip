@@ -18,7 +18,8 @@
 // Pass 2 (columns, in place): a block stages a strip of G columns x L rows
 //   through LDS (rows of G*8 contiguous bytes), each group transforms one
 //   column in registers, scales by 1/L^2 and the strip is written back.
-// HBM: 2 x 2 x 8 L^2 bytes per patch per iteration.
+// HBM: at most 2 x 2 x 8 L^2 bytes per patch per iteration; only the live band
+// of the spectrum (fpm_state.hpp) is read in pass 1 and re-read in pass 2.
 #include <hip/hip_runtime.h>
 
 #include "dft16.hpp"
