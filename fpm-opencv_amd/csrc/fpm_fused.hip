@@ -322,6 +322,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         for (int j = 0; j < RPG; ++j)
 #pragma unroll
             for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(sr, j, s);
+        if (towner) Ot = sr[tp.x * L + tp.y];
     }
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
@@ -329,11 +330,9 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         float2 *srow = spec + (unsigned)(yc * L + xc);   // spec[yc + ky][xc + kx] = srow[ky*L + kx]
         const float *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
 
-        // ---- gather the sub-aperture on the support (pre-update Objfcrop, fpmMain.cpp:358-362)
-        if (towner) {
-            Ot = srow[tp.x * L + tp.y];
-            tailX[tid] = cmul(Ot, Pt);
-        }
+        // ---- gather the sub-aperture on the support (pre-update Objfcrop,
+        // fpmMain.cpp:358-362); the tail pixels' O was loaded with Opre
+        if (towner) tailX[tid] = cmul(Ot, Pt);
         __syncthreads();  // tailX
         FPM_STAMP(0)
 
@@ -572,6 +571,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
                 for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(sr, j, s);
+            if (towner) Ot = sr[tp.x * L + tp.y];
         }
         FPM_STAMP(4)
 
