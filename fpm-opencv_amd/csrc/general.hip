@@ -290,12 +290,21 @@ __device__ __forceinline__ void fft_inplace_pass(float2 *buf, int n, int lc, int
     __syncthreads();
 }
 
+// Input band of a batched transform: sequences gs outside [qlo, qhi] and
+// elements gi with (gi + eroll) mod n outside [elo, ehi] are known to be
+// exactly zero and are not read (objCrop over the spectrum's live band,
+// fpm_state.hpp); the default covers everything.
+struct FftBand {
+    int qlo = 0, qhi = 0x7fffffff, elo = 0, ehi = 0x7fffffff, eroll = 0;
+};
+
 template <bool INV>
 __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, float2 *out, FftPlan pl,
                                                            const float2 *__restrict__ tw, int lc, int nseq,
                                                            size_t in_bs, int in_ss, int in_es, size_t out_bs,
                                                            int out_ss, int out_es, int sroll, int iroll,
-                                                           float scale, const __half2 *in16, float in16_scale) {
+                                                           float scale, const __half2 *in16, float in16_scale,
+                                                           FftBand band) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const int n = pl.n, C = 1 << lc, cm = C - 1;
     const int s0 = blockIdx.x << lc, b = blockIdx.y;
@@ -325,10 +334,13 @@ __global__ void __launch_bounds__(kFftThreads) k_fft_batch(const float2 *in, flo
             if (colmajor) { sq = idx & cm; i = idx >> lc; }
             else { sq = udiv(idx, n, rn); i = idx - sq * n; }
             at[q] = sq * lss + i * les;
-            if (sq < cs) {
-                int gs = s0 + sq + sroll, gi = i + iroll;
-                if (gs >= nseq) gs -= nseq;
-                if (gi >= n) gi -= n;
+            int gs = s0 + sq + sroll, gi = i + iroll;
+            if (gs >= nseq) gs -= nseq;
+            if (gi >= n) gi -= n;
+            int eb = gi + band.eroll;
+            if (eb >= n) eb -= n;
+            // outside the band the input is exactly zero: skip the load
+            if (sq < cs && gs >= band.qlo && gs <= band.qhi && eb >= band.elo && eb <= band.ehi) {
                 const size_t ii = (size_t)gs * in_ss + (size_t)gi * in_es;
                 if (in16) {  // fp16-stored spectrum (config 5): widen, undo the storage scale
                     const float2 f = __half22float2(in16[ii]);
@@ -873,7 +885,7 @@ int fft_max_len() { return fft_pass_capacity(5); }  // the smallest of the radix
 hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const FftPlan &pl, const float2 *tw,
                             int nseq, int B, size_t in_bs, int in_ss, int in_es, size_t out_bs, int out_ss,
                             int out_es, int sroll, int iroll, float scale, hipStream_t s,
-                            const __half2 *in16 = nullptr, float in16_scale = 1.f) {
+                            const __half2 *in16 = nullptr, float in16_scale = 1.f, FftBand band = FftBand()) {
     const int lc = fft_log2_seq_per_block(pl);
     if (lc < 0) return hipErrorInvalidValue;
     const int C = 1 << lc;
@@ -885,10 +897,10 @@ hipError_t launch_fft_batch(bool inverse, const float2 *in, float2 *out, const F
     if (e != hipSuccess) return e;
     if (inverse)
         hipLaunchKernelGGL(k_fft_batch<true>, grid, dim3(kFftThreads), lds, s, in, out, pl, tw, lc, nseq, in_bs,
-                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale, in16, in16_scale);
+                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale, in16, in16_scale, band);
     else
         hipLaunchKernelGGL(k_fft_batch<false>, grid, dim3(kFftThreads), lds, s, in, out, pl, tw, lc, nseq, in_bs,
-                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale, in16, in16_scale);
+                           in_ss, in_es, out_bs, out_ss, out_es, sroll, iroll, scale, in16, in16_scale, band);
     return hipGetLastError();
 }
 
@@ -929,11 +941,21 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
     }
     const int L = st.L;
     const size_t bs = (size_t)L * L;
+    // rows: spec rows (sequences) and columns (elements) outside the live band
+    // are zero; columns: objF row i of the intermediate is spec row i + L/2
+    FftBand rows, cols;
+    rows.qlo = st.sy0;
+    rows.qhi = st.sy1;
+    rows.elo = st.sx0;
+    rows.ehi = st.sx1;
+    cols.elo = st.sy0;
+    cols.ehi = st.sy1;
+    cols.eroll = L / 2;
     hipError_t e = launch_fft_batch(true, st.spec, out, pl_L, tw_L, L, st.B, bs, L, 1, bs, L, 1, L / 2, L / 2, 1.f,
-                                    s, st.spec16, st.hinv);
+                                    s, st.spec16, st.hinv, rows);
     if (e != hipSuccess) return e;
     return launch_fft_batch(true, out, out, pl_L, tw_L, L, st.B, bs, 1, L, bs, 1, L, 0, 0,
-                            1.0f / ((float)L * (float)L), s);
+                            1.0f / ((float)L * (float)L), s, nullptr, 1.f, cols);
 }
 
 }  // namespace fpm
