@@ -252,6 +252,12 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     st.delta1 = (float)prob->delta1;
     st.delta2 = (float)prob->delta2;
     st.eps = (float)prob->eps;
+    {   // cv::add(UMat CV_64FC2, double) semantics (fpm_hip.h FPM_FLAG_SCALAR_RE_ONLY)
+        const bool re_only = (prob->flags & FPM_FLAG_SCALAR_RE_ONLY) != 0;
+        st.eps_im = re_only ? 0.f : st.eps;
+        st.d1_im = re_only ? 0.f : st.delta1;
+        st.d2_im = re_only ? 0.f : st.delta2;
+    }
     make_plan(np, &c->pl_np);
     make_plan(L, &c->pl_L);
     // live band of the centred spectrum (fpm_state.hpp): the init placement at

@@ -10,7 +10,8 @@
 //     A  row IDFTs of the box rows of O*P (:364-365), the half's 128
 //        outputs -> LDS half-T (64 FFT rows + <= 8 "tail" rows by direct sums)
 //     B  per column x: column IDFT (only box rows are non-zero), 1/Np^2,
-//        psi' = sqrt(I) psi/|psi + eps| (eps on Re), column DFT, keep the box
+//        psi' = sqrt(I) psi/|psi + eps| (eps on Re and Im),
+//        column DFT, keep the box
 //        rows -> half-T in place                                   (:365-394)
 //     C  row DFTs of the half rows, output-pruned to the support columns,
 //        accumulated over the two halves in registers              (:394)
@@ -293,6 +294,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
     float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
     float pm = st.pmax[b];
     const float epsn = st.eps * (float)(NP * NP);  // eps on the unscaled IDFT
+    const float epsn_im = st.eps_im * (float)(NP * NP);
     __syncthreads();
 
     // diagnostic: shader-clock cycles per phase, summed over LEDs (wave-uniform)
@@ -442,8 +444,9 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 for (int m2 = 0; m2 < 16; ++m2) {
                     const float invI = __uint_as_float(iw[m2]);
                     // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
-                    const float tre = r[m2].x + epsn;
-                    const float mag2 = __builtin_fmaf(tre, tre, r[m2].y * r[m2].y);
+                    // (cv::add(UMat c2, double) puts eps on both channels, :390)
+                    const float tre = r[m2].x + epsn, tim = r[m2].y + epsn_im;
+                    const float mag2 = __builtin_fmaf(tre, tre, tim * tim);
                     const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
                     v[m2] = make_float2(r[m2].x * sc, r[m2].y * sc);
                 }
@@ -539,13 +542,15 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 const int kx = slot_kx(t, s);
                 const float2 p = P[j][s], o = Opre[j][s];
                 const float2 D = csub(F[j][s], cmul(o, p));   // Objfup - ObjfcropP (:409)
+                // D |P| P* / ((|P|^2 + d2 + i d2im) max|P|)  (:406-419)
                 const float pa = cmag(p);
-                const float rin = __builtin_amdgcn_rcpf((pa * pa + st.delta2) * pm);
-                const float2 nv = cadd(o, cscale(cmul(D, cscale(cconj(p), pa)), rin));
+                const float2 kin = upd_coef(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm);
+                const float2 nv = cadd(o, cmul(cmul(D, cscale(cconj(p), pa)), kin));
+                // D |O| O* / (|O|^2 + d1 + i d1im); / max|objF| at the commit (:459-471)
                 const float oa = cmag(o);
-                const float rip = __builtin_amdgcn_rcpf(oa * oa + st.delta1);
+                const float2 kip = upd_coef(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f);
                 // this group's own half-T row is no longer read: park the numerator there
-                th[(g + NG * j) * TLD + s * 16 + t] = cscale(cmul(D, cscale(cconj(o), oa)), rip);
+                th[(g + NG * j) * TLD + s * 16 + t] = cmul(cmul(D, cscale(cconj(o), oa)), kip);
                 if ((inmask[j] >> s) & 1) {
                     srow[kyr[j] * L + kx] = nv;
                     note(yc + kyr[j], xc + kx, oa, cmag(nv));
@@ -555,12 +560,12 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             const float2 p = Pt, o = Ot;
             const float2 D = csub(tailF[tid], tailX[tid]);
             const float pa = cmag(p);
-            const float rin = __builtin_amdgcn_rcpf((pa * pa + st.delta2) * pm);
-            const float2 nv = cadd(o, cscale(cmul(D, cscale(cconj(p), pa)), rin));
+            const float2 kin = upd_coef(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm);
+            const float2 nv = cadd(o, cmul(cmul(D, cscale(cconj(p), pa)), kin));
             srow[tp.x * L + tp.y] = nv;
             const float oa = cmag(o);
-            const float rip = __builtin_amdgcn_rcpf(oa * oa + st.delta1);
-            NPt = cscale(cmul(D, cscale(cconj(o), oa)), rip);
+            const float2 kip = upd_coef(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f);
+            NPt = cmul(cmul(D, cscale(cconj(o), oa)), kip);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
         FPM_STAMP(9)

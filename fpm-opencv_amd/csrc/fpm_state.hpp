@@ -52,6 +52,11 @@ struct DevState {
     int np, L, r, nb, B, ntx, nty;
     int npart;        // partial max|P| values per patch
     float delta1, delta2, eps;
+    // imaginary parts of the scalars the reference adds with cv::add(UMat c2,
+    // double) (fpmMain.cpp:390,417,469): OpenCV unrolls a double into every
+    // channel, so these equal eps / delta1 / delta2 by default and are 0 under
+    // FPM_FLAG_SCALAR_RE_ONLY.  Update denominators are (a + i c) * max.
+    float eps_im, d1_im, d2_im;
     float hscale, hinv;  // fp16 storage scale and its inverse (powers of two)
     // live band of the centred spectrum, inclusive: spec is zeroed by fpm_init
     // and only ever changes on the support boxes of the init placement
@@ -75,6 +80,19 @@ __device__ __forceinline__ void spec_st(const DevState &st, int b, size_t i, flo
         st.spec16[o] = __float22half2_rn(make_float2(v.x * st.hscale, v.y * st.hscale));
     else
         st.spec[o] = v;
+}
+
+// ePIE update coefficient 1 / ((a + i c) m) = (a - i c) / ((a^2 + c^2) m) for
+// the complex denominators of fpmMain.cpp:417-419 / :469-471 (c = 0 under
+// FPM_FLAG_SCALAR_RE_ONLY).  a = |X|^2 + delta >= delta > 0.
+__device__ __forceinline__ float2 upd_coef(float a, float c, float m) {
+    const float ri = __builtin_amdgcn_rcpf(__builtin_fmaf(a, a, c * c) * m);
+    return make_float2(a * ri, -c * ri);
+}
+// IEEE-division variant for the general path
+__device__ __forceinline__ float2 upd_coef_div(float a, float c, float m) {
+    const float d = __builtin_fmaf(a, a, c * c) * m;
+    return make_float2(a / d, -c / d);
 }
 
 }  // namespace fpm

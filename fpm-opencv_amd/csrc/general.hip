@@ -77,14 +77,14 @@ __global__ void __launch_bounds__(256) k_colpass(DevState st, StepArgs sa, FftPl
     float2 *res = stockham<true>(bufa, bufb, 1, pl, tw, threadIdx.x, blockDim.x);
     float2 *oth = (res == bufa) ? bufb : bufa;
     // amplitude replacement, fpmMain.cpp:378-393:
-    //   psi = ifft2(.) (1/Np^2 scale), psi' = sqrt(I) * psi / |psi + eps| (eps on Re)
+    //   psi = ifft2(.) (1/Np^2 scale), psi' = sqrt(I) * psi / |psi + eps| (eps on Re and Im)
     const float inv_n2 = 1.0f / ((float)np * (float)np);
     const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
     for (int y = threadIdx.x; y < np; y += blockDim.x) {
         float2 psi = cscale(res[y], inv_n2);
         float a = sqrtf((float)I[(size_t)y * np + x]);
-        float tre = psi.x + st.eps;
-        float mag = sqrtf(tre * tre + psi.y * psi.y);
+        float tre = psi.x + st.eps, tim = psi.y + st.eps_im;
+        float mag = sqrtf(tre * tre + tim * tim);
         float s = a / mag;
         res[y] = make_float2(psi.x * s, psi.y * s);
     }
@@ -125,14 +125,11 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
         const float2 D = csub(F, cmul(o, p));    // Objfup - ObjfcropP (:409,463)
         // object update (:406-419,433): D |P| P* / ((|P|^2 + d2) max|P|)
         const float pa = cmag(p);
-        const float den_o = (pa * pa + st.delta2) * pm;
-        const float2 dpc = cmul(D, cscale(cconj(p), pa));
-        spec_st(st, b, si, make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o));
+        const float2 dpc = cmul(cmul(D, cscale(cconj(p), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
+        spec_st(st, b, si, cadd(o, dpc));
         // pupil numerator (:459-464,469): D |O| O* / (|O|^2 + d1); max|objF| in K4
         const float oa = cmag(o);
-        const float den_p = oa * oa + st.delta1;
-        const float2 n = cmul(D, cscale(cconj(o), oa));
-        dP[row * nb + j] = make_float2(n.x / den_p, n.y / den_p);
+        dP[row * nb + j] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
     }
 }
 
@@ -494,13 +491,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16
         const float2 F = tile[c * lss + (kx < 0 ? kx + np : kx)];  // Objfup (:394)
         const float2 D = csub(F, cmul(o, p));                   // Objfup - ObjfcropP (:409,463)
         const float pa = cmag(p);                               // object update (:406-419,433)
-        const float den_o = (pa * pa + st.delta2) * pm;
-        const float2 dpc = cmul(D, cscale(cconj(p), pa));
-        spec_st(st, b, si, make_float2(o.x + dpc.x / den_o, o.y + dpc.y / den_o));
+        const float2 dpc = cmul(cmul(D, cscale(cconj(p), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
+        spec_st(st, b, si, cadd(o, dpc));
         const float oa = cmag(o);                               // pupil numerator (:459-464,469)
-        const float den_p = oa * oa + st.delta1;
-        const float2 n = cmul(D, cscale(cconj(o), oa));
-        dP[row * nb + j] = make_float2(n.x / den_p, n.y / den_p);
+        dP[row * nb + j] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
     }
 }
 
@@ -540,8 +534,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16
         if (c >= cs) continue;
         const float2 psi = cscale(tile[idx], inv_n2);
         const float a = sqrtf((float)I[(size_t)y * np + x0 + c]);
-        const float tre = psi.x + st.eps;
-        const float mag = sqrtf(tre * tre + psi.y * psi.y);
+        const float tre = psi.x + st.eps, tim = psi.y + st.eps_im;
+        const float mag = sqrtf(tre * tre + tim * tim);
         const float sc = a / mag;
         tile[idx] = make_float2(psi.x * sc, psi.y * sc);
     }
@@ -701,8 +695,8 @@ k_colpass_wave(DevState st, StepArgs sa, FftPlan pl, const float2 *__restrict__ 
             float2 *e = wb + c * P + y;
             const float2 psi = cscale(*e, inv_n2);
             const float a = sqrtf((float)iv[q * CW + c]);
-            const float tre = psi.x + st.eps;
-            const float mag = sqrtf(tre * tre + psi.y * psi.y);
+            const float tre = psi.x + st.eps, tim = psi.y + st.eps_im;
+            const float mag = sqrtf(tre * tre + tim * tim);
             const float sc = a / mag;
             *e = make_float2(psi.x * sc, psi.y * sc);
         }

@@ -31,6 +31,7 @@ FPM_ERR_NODEV = -19
 PATH_AUTO, PATH_GENERAL, PATH_FUSED = 0, 1, 2
 FLAG_OBJCROP_LAST_ONLY = 1
 FLAG_SPEC_FP16 = 2          # fp16 spectrum storage, fp32 arithmetic (config 5)
+FLAG_SCALAR_RE_ONLY = 4     # legacy: cv::add(UMat c2, double) on the real channel only (fpm_hip.h)
 
 # every symbol include/fpm_hip.h declares
 HIP_SYMBOLS = (

@@ -75,6 +75,19 @@ typedef struct fpm_frames {
                                           storage / fp32 accumulate"); general
                                           path only.  The reference keeps
                                           CV_64FC2 objF (fpmMain.h:92) */
+#define FPM_FLAG_SCALAR_RE_ONLY    4u  /* legacy semantics for the reference's
+                                          cv::add / cv::multiply(UMat CV_64FC2,
+                                          double) at fpmMain.cpp:390,417-418,
+                                          469-470: the scalar touches the real
+                                          channel only.  Default (flag clear) is
+                                          OpenCV's published behaviour: a double
+                                          becomes a 1x1 array that arithm_op's
+                                          convertAndUnrollScalar replicates into
+                                          EVERY channel, so eps is added to Re and
+                                          Im and the update denominators are
+                                          complex, ((|P|^2+d2) + i d2) max|P| and
+                                          ((|O|^2+d1) + i d1) max|objF| (DESIGN.md
+                                          section 2) */
 
 /*
  * Problem description: the FPM_Dataset fields runFPM reads

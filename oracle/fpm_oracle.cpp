@@ -10,8 +10,13 @@
 //   - element-wise complex ops as separate passes (:364-475),
 //   - the per-iteration objCrop IDFT (:481).
 // The DFTs are this file's own mixed-radix (2/3/4/5) Stockham FFT in double.
-// cvComplex semantics assumed as in SURVEY.md 8(c)(i)-(vii) (parity unpinned
-// at that boundary: the library is not in the reference tree).
+// cvComplex semantics assumed as in SURVEY.md 8(c)(i)-(iii),(v)-(vii) (parity
+// unpinned at that boundary: the library is not in the reference tree).
+// (iv) is replaced by OpenCV's published scalar rule: cv::add / cv::multiply
+// (UMat CV_64FC2, double) unroll the double into every channel (arithm_op ->
+// checkScalar -> convertAndUnrollScalar), so eps lands on Re and Im (:390)
+// and the update denominators are complex (:417-418, :469-470).  all_ch = 0
+// restates the real-channel-only assumption (FPM_FLAG_SCALAR_RE_ONLY).
 //
 // C ABI (ctypes from tests / bench):
 //   int oracle_run_fpm(...)        one patch
@@ -118,6 +123,7 @@ struct Params {
     const uint16_t *stack;
     const int *order, *x0, *y0;
     double d1, d2, eps;
+    int all_ch;  // 1: cv::add(c2, double) acts on both channels (OpenCV default)
 };
 
 int run_one(const Params &P, double *objF_out, double *objCrop_out, double *pupil_out) {
@@ -169,7 +175,8 @@ int run_one(const Params &P, double *objF_out, double *objCrop_out, double *pupi
             for (size_t i = 0; i < NN; ++i) amp[i] = cplx(std::sqrt((double)I[i]), 0.0);
             // :390-394
             tmp.resize(NN);
-            for (size_t i = 0; i < NN; ++i) tmp[i] = objcropP[i] + cplx(P.eps, 0.0);
+            const double sim = P.all_ch ? 1.0 : 0.0;  // imaginary share of a cv::add scalar
+            for (size_t i = 0; i < NN; ++i) tmp[i] = objcropP[i] + cplx(P.eps, sim * P.eps);
             for (size_t i = 0; i < NN; ++i) tmp[i] = cplx(std::abs(tmp[i]), 0.0);
             for (size_t i = 0; i < NN; ++i) tmp[i] = objcropP[i] / tmp[i];
             for (size_t i = 0; i < NN; ++i) tmp[i] = tmp[i] * amp[i];
@@ -185,7 +192,7 @@ int run_one(const Params &P, double *objF_out, double *objCrop_out, double *pupi
             for (size_t i = 0; i < NN; ++i) dO[i] = objfup[i] - objfcropP[i];
             for (size_t i = 0; i < NN; ++i) num[i] = dO[i] * num[i];
             for (size_t i = 0; i < NN; ++i) pmax = std::max(pmax, pabs[i].real());
-            for (size_t i = 0; i < NN; ++i) dO[i] = cplx((pabs[i] * pabs[i]).real() + P.d2, 0.0) * pmax;
+            for (size_t i = 0; i < NN; ++i) dO[i] = ((pabs[i] * pabs[i]) + cplx(P.d2, sim * P.d2)) * pmax;
             for (size_t i = 0; i < NN; ++i) dO[i] = num[i] / dO[i];
             // :427-447
             fftshift(objF, objFc, L, L);
@@ -207,7 +214,7 @@ int run_one(const Params &P, double *objF_out, double *objCrop_out, double *pupi
             for (size_t i = 0; i < NN; ++i) dP[i] = objfup[i] - objfcropP[i];
             for (size_t i = 0; i < NN; ++i) num[i] = dP[i] * num[i];
             for (size_t i = 0; i < LL; ++i) omax = std::max(omax, objf_abs[i]);
-            for (size_t i = 0; i < NN; ++i) dP[i] = cplx((oabs[i] * oabs[i]).real() + P.d1, 0.0) * omax;
+            for (size_t i = 0; i < NN; ++i) dP[i] = ((oabs[i] * oabs[i]) + cplx(P.d1, sim * P.d1)) * omax;
             for (size_t i = 0; i < NN; ++i) dP[i] = num[i] / dP[i];
             for (size_t i = 0; i < NN; ++i) dP[i] = dP[i] * support[i];
             for (size_t i = 0; i < NN; ++i) pupil[i] = pupil[i] + dP[i];
@@ -236,8 +243,8 @@ extern "C" {
 // stack: uint16 [n_stack][Np][Np]; outputs complex128 interleaved (may be NULL)
 int oracle_run_fpm(int np, int L, int n_stack, const uint16_t *stack, int n_order, const int *order,
                    const int *x0, const int *y0, int radius, double delta1, double delta2, double eps, int iters,
-                   double *objF, double *objCrop, double *pupil) {
-    Params P{np, L, n_stack, n_order, radius, iters, stack, order, x0, y0, delta1, delta2, eps};
+                   int all_channels, double *objF, double *objCrop, double *pupil) {
+    Params P{np, L, n_stack, n_order, radius, iters, stack, order, x0, y0, delta1, delta2, eps, all_channels};
     return run_one(P, objF, objCrop, pupil);
 }
 
@@ -245,7 +252,8 @@ int oracle_run_fpm(int np, int L, int n_stack, const uint16_t *stack, int n_orde
 // patches are spread over n_threads std::threads.  Outputs per patch.
 int oracle_run_fpm_batch(int np, int L, int n_stack, int n_patch, const uint16_t *stack, int n_order,
                          const int *order, const int *x0, const int *y0, int radius, double delta1, double delta2,
-                         double eps, int iters, int n_threads, double *objF, double *objCrop, double *pupil) {
+                         double eps, int iters, int all_channels, int n_threads, double *objF, double *objCrop,
+                         double *pupil) {
     const size_t NN = (size_t)np * np, LL = (size_t)L * L;
     std::vector<int> rc(n_patch, 0);
     auto work = [&](int t) {
@@ -253,7 +261,8 @@ int oracle_run_fpm_batch(int np, int L, int n_stack, int n_patch, const uint16_t
         for (int b = t; b < n_patch; b += n_threads) {
             for (int s = 0; s < n_stack; ++s)
                 std::memcpy(&own[(size_t)s * NN], stack + ((size_t)s * n_patch + b) * NN, NN * sizeof(uint16_t));
-            Params P{np, L, n_stack, n_order, radius, iters, own.data(), order, x0, y0, delta1, delta2, eps};
+            Params P{np, L, n_stack, n_order, radius, iters, own.data(), order, x0, y0, delta1, delta2, eps,
+                     all_channels};
             rc[b] = run_one(P, objF ? objF + 2 * LL * b : nullptr, objCrop ? objCrop + 2 * LL * b : nullptr,
                             pupil ? pupil + 2 * NN * b : nullptr);
         }

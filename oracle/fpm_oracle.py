@@ -19,8 +19,14 @@ side by side with the reference:
 Semantics of the un-vendored ``cvComplex`` helpers are *assumed* as listed in
 SURVEY.md section 8(c) (i)-(vii): ``fft2`` = unscaled forward DFT, ``ifft2`` =
 inverse DFT scaled by 1/N, ``complexAbs`` returns (|z|, 0), ``fftShift`` is a
-quadrant swap (even sizes only), ``cv::add(UMat, double)`` adds to the real
-channel only, the filled ``cv::circle`` is the Euclidean disk.  The reference
+quadrant swap (even sizes only), the filled ``cv::circle`` is the Euclidean
+disk.  ``cv::add`` / ``cv::multiply(UMat CV_64FC2, double)`` (fpmMain.cpp:390,
+417-418, 469-470) follow OpenCV's published ``arithm_op``: the double becomes
+a 1x1 array (``_InputArray(const double&)``), ``checkScalar`` accepts it as a
+scalar and ``convertAndUnrollScalar`` copies it into EVERY channel, so eps is
+added to Re and Im and both update denominators are complex
+(``all_channels=True``, the default).  ``all_channels=False`` restates the
+round-1 assumption (real channel only), kept as FPM_FLAG_SCALAR_RE_ONLY.  The reference
 cannot be built here (OpenCV 3 + cvComplex absent), so these semantics are
 "parity unpinned" at the cvComplex boundary; see DESIGN.md "Oracle".
 """
@@ -68,7 +74,8 @@ def _ifft2(a):
 
 def run_fpm(stack, order, x0, y0, np_: int, L: int, radius: int,
             delta1: float, delta2: float, iters: int,
-            eps: float = float(np.float32(1e-10)), record=None):
+            eps: float = float(np.float32(1e-10)), record=None,
+            all_channels: bool = True):
     """Restatement of ``runFPM`` (fpmMain.cpp:274-498) for ONE patch.
 
     Parameters mirror the ``FPM_Dataset`` fields runFPM reads
@@ -81,13 +88,18 @@ def run_fpm(stack, order, x0, y0, np_: int, L: int, radius: int,
               in the *centred* L x L spectrum.
     radius  : ``naRadius`` (fpmMain.cpp:305-306).
     delta1/2: JSON ``asInt`` values (fpmMain.cpp:567-568).
-    eps     : ``float eps = 1e-10`` (fpmMain.h:99), added to Re only.
+    eps     : ``float eps = 1e-10`` (fpmMain.h:99).
+    all_channels : OpenCV scalar unrolling (module docstring): a double added
+              to / multiplied into a CV_64FC2 array acts on both channels.
 
     Returns dict(objF=un-centred L x L spectrum, objCrop=IDFT(objF)/L^2,
     pupil=centred Np x Np pupil (fpmMain.cpp:496), support=un-centred S).
     """
     stack = np.asarray(stack)
     order = [int(i) for i in order]
+    # cv::add(c2, s) with s a double: (re + s, im + s) when unrolled to every
+    # channel, (re + s, im) under the real-channel-only assumption
+    cs = (1 + 1j) if all_channels else 1.0
     S = disk_support(np_, radius)                       # :302-313
     pupil = S.astype(np.complex128)                     # mergeUMat(planes)
     support = pupil.copy()                              # :313
@@ -113,7 +125,7 @@ def run_fpm(stack, order, x0, y0, np_: int, L: int, radius: int,
             objfcropP = objfcrop * pupil                                # :364
             objcropP = _ifft2(objfcropP)                                # :365
             object_amp = np.sqrt(stack[led].astype(np.float64))         # :378-387
-            tmp1 = objcropP + eps                                       # :390 (Re only)
+            tmp1 = objcropP + eps * cs                                  # :390
             tmp3 = np.abs(tmp1)                                         # :391
             tmp1 = objcropP / tmp3                                      # :392
             tmp3 = tmp1 * object_amp                                    # :393
@@ -123,7 +135,7 @@ def run_fpm(stack, order, x0, y0, np_: int, L: int, radius: int,
             pupil_abs = np.abs(pupil)
             numerator = (objfup - objfcropP) * (pupil_abs * np.conj(pupil))
             pupil_abs_max = pupil_abs.max()                             # :415
-            denom = (pupil_abs * pupil_abs + delta2) * pupil_abs_max
+            denom = (pupil_abs * pupil_abs + delta2 * cs) * pupil_abs_max  # :417-418
             tmp2 = numerator / denom                                    # :419
             objF_c = fftshift2(objF)                                    # :427
             upd = fftshift2(tmp2) + objF_c[ys:ys + np_, xs:xs + np_]    # :432-433
@@ -134,7 +146,7 @@ def run_fpm(stack, order, x0, y0, np_: int, L: int, radius: int,
             objfcrop_abs = np.abs(objfcrop)
             objf_abs_max = np.abs(objF).max()                           # :460,467
             numerator = (objfup - objfcropP) * (objfcrop_abs * np.conj(objfcrop))
-            denom = (objfcrop_abs * objfcrop_abs + delta1) * objf_abs_max
+            denom = (objfcrop_abs * objfcrop_abs + delta1 * cs) * objf_abs_max  # :469-470
             tmp2 = (numerator / denom) * support                        # :471-472
             pupil = pupil + tmp2                                        # :475
             if record is not None:

@@ -19,10 +19,10 @@ def load():
         lib = C.CDLL(ORACLE_SO)
         ip, dp, u16p = C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_uint16)
         lib.oracle_run_fpm.argtypes = [C.c_int, C.c_int, C.c_int, u16p, C.c_int, ip, ip, ip, C.c_int,
-                                       C.c_double, C.c_double, C.c_double, C.c_int, dp, dp, dp]
+                                       C.c_double, C.c_double, C.c_double, C.c_int, C.c_int, dp, dp, dp]
         lib.oracle_run_fpm_batch.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, u16p, C.c_int, ip, ip, ip,
                                              C.c_int, C.c_double, C.c_double, C.c_double, C.c_int, C.c_int,
-                                             dp, dp, dp]
+                                             C.c_int, dp, dp, dp]
         lib.oracle_fft2.argtypes = [dp, C.c_int, C.c_int, C.c_int]
         _lib = lib
     return _lib
@@ -32,8 +32,9 @@ def _ip(a):
     return a.ctypes.data_as(C.POINTER(C.c_int))
 
 
-def run_fpm(stack, order, x0, y0, np_, L, r, d1, d2, iters, eps=float(np.float32(1e-10))):
-    """One patch; stack uint16 [n_stack][Np][Np]. Returns complex128 outputs."""
+def run_fpm(stack, order, x0, y0, np_, L, r, d1, d2, iters, eps=float(np.float32(1e-10)), all_channels=True):
+    """One patch; stack uint16 [n_stack][Np][Np]. Returns complex128 outputs.
+    all_channels=False restates FPM_FLAG_SCALAR_RE_ONLY (fpm_oracle.cpp header)."""
     lib = load()
     st = np.ascontiguousarray(stack, np.uint16)
     order, x0, y0 = (np.ascontiguousarray(v, np.int32) for v in (order, x0, y0))
@@ -42,14 +43,14 @@ def run_fpm(stack, order, x0, y0, np_, L, r, d1, d2, iters, eps=float(np.float32
     pupil = np.zeros((np_, np_), np.complex128)
     dp = C.POINTER(C.c_double)
     rc = lib.oracle_run_fpm(np_, L, len(x0), st.ctypes.data_as(C.POINTER(C.c_uint16)), len(order), _ip(order),
-                            _ip(x0), _ip(y0), r, d1, d2, eps, iters, objF.ctypes.data_as(dp),
+                            _ip(x0), _ip(y0), r, d1, d2, eps, iters, int(all_channels), objF.ctypes.data_as(dp),
                             objCrop.ctypes.data_as(dp), pupil.ctypes.data_as(dp))
     assert rc == 0, rc
     return dict(objF=objF, objCrop=objCrop, pupil=pupil)
 
 
 def run_fpm_batch(stack, order, x0, y0, np_, L, r, d1, d2, iters, threads, outputs=True,
-                  eps=float(np.float32(1e-10))):
+                  eps=float(np.float32(1e-10)), all_channels=True):
     """stack uint16 [n_stack][B][Np][Np]; B patches on `threads` threads."""
     lib = load()
     st = np.ascontiguousarray(stack, np.uint16)
@@ -58,7 +59,7 @@ def run_fpm_batch(stack, order, x0, y0, np_, L, r, d1, d2, iters, threads, outpu
     dp = C.POINTER(C.c_double)
     objCrop = np.zeros((B, L, L), np.complex128) if outputs else None
     rc = lib.oracle_run_fpm_batch(np_, L, len(x0), B, st.ctypes.data_as(C.POINTER(C.c_uint16)), len(order),
-                                  _ip(order), _ip(x0), _ip(y0), r, d1, d2, eps, iters, threads, None,
+                                  _ip(order), _ip(x0), _ip(y0), r, d1, d2, eps, iters, int(all_channels), threads, None,
                                   objCrop.ctypes.data_as(dp) if outputs else None, None)
     assert rc == 0, rc
     return objCrop

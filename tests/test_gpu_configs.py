@@ -1,12 +1,22 @@
-"""BASELINE.json configs 1-2 as parity cases (GPU only): dataset_mono optics
-with the 508-LED dome table (SURVEY.md 8(c) fallback; geometry and LED order
-from the reference's own jsoncpp probe, tests/golden/geometry_mono_dome.json):
-Np 90, L 360, naRadius 30, 193 LEDs -- the general (mixed radix 2/3/5) path.
+"""BASELINE.json configs 1-5 as parity cases (GPU only).
 
-  config 1: 1 patch, 5 iterations, vs the C++ fp64 oracle
-  config 2: 64 patches batched on one GPU; sampled patches vs the oracle
+  config 1: dataset_mono optics with the 508-LED dome table (SURVEY.md 8(c)
+            fallback; geometry and LED order from the reference's own jsoncpp
+            probe, tests/golden/geometry_mono_dome.json): Np 90, L 360,
+            naRadius 30, 193 LEDs, 1 patch, 5 iterations, vs the C++ fp64
+            oracle, for both readings of cv::add(UMat c2, double)
+  config 2: the same geometry, 64 patches batched, 2 iterations; sampled
+            patches vs the oracle
+  config 3: dataset_dogStomach.json literal (tests/golden/
+            geometry_dogStomach_literal.json: 157 LEDs in the reference's
+            tie-ordered std::sort order, Np 200, L 600, naRadius 26,
+            delta1/delta2 = 10/3), 256 patches, 2 iterations; patches
+            0/128/255 vs the oracle
+  config 4: one GPU's shard of the 1024-patch metric field (128 patches x
+            293 LEDs, Np 256, L 768), 1 iteration; sampled patches vs oracle
+  config 5: Np 1024, L 4096 (fp32 and fp16 spectrum storage)
 Tolerance: relative L2 <= 1e-4 after 5 iterations (SURVEY.md 8(c) proposes
-1e-3), <= 1e-5 after 1 iteration.
+1e-3), <= 1e-5 after 1 iteration, <= 5e-5 after 2.
 """
 import json
 import os
@@ -32,15 +42,18 @@ def _geometry():
     return p, x0, y0
 
 
-def test_config1_mono_dome_single_patch_5_iterations():
+@pytest.mark.parametrize("all_channels", [True, False], ids=["opencv_scalar", "re_only"])
+def test_config1_mono_dome_single_patch_5_iterations(all_channels):
     import oracle_lib
     p, x0, y0 = _geometry()
     Np, L, r = p["np"], p["nlarge"], p["na_radius"]
     assert (Np, L, r, len(x0)) == (90, 360, 30, 193)
     order = np.arange(len(x0))
     stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=11)
-    ref = oracle_lib.run_fpm(stack[:, 0], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 5)
-    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=1)
+    ref = oracle_lib.run_fpm(stack[:, 0], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 5,
+                             all_channels=all_channels)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=1,
+                           flags=0 if all_channels else fpm_amd.FLAG_SCALAR_RE_ONLY)
     out = fpm_amd.run_fpm(prob, stack, 5)
     for k in ("objCrop", "objF", "pupil"):
         e = rel_l2(out[k][0], ref[k])
@@ -55,12 +68,77 @@ def test_config2_mono_dome_64_patches_batched():
     B = 64
     stack = make_stack(Np, L, r, x0, y0, n_patch=B, seed=12)
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=B)
-    out = fpm_amd.run_fpm(prob, stack, 1)
+    out = fpm_amd.run_fpm(prob, stack, 2)
     assert np.isfinite(out["objCrop"]).all()
-    for b in (0, 37, 63):
-        ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 1)
-        assert rel_l2(out["objCrop"][b], ref["objCrop"]) < 1e-5
-        assert rel_l2(out["pupil"][b], ref["pupil"]) < 1e-5
+    sample = (0, 37, 63)
+    refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 2,
+                                    threads=3)
+    for i, b in enumerate(sample):
+        assert rel_l2(out["objCrop"][b], refs[i]) < 5e-5, b
+
+
+def _probe_geometry(name):
+    p = json.load(open(os.path.join(os.path.dirname(__file__), "golden", name)))["probe"]
+    leds = {l["led"]: l for l in p["leds"]}
+    order = p["sorted_indices"]
+    x0 = np.array([leds[n]["crop_x0"] for n in order], np.int32)
+    y0 = np.array([leds[n]["crop_y0"] for n in order], np.int32)
+    return p, x0, y0
+
+
+def _tiled_stack(Np, L, r, x0, y0, B, n_distinct, seed):
+    """[nLED][B][Np][Np]: n_distinct forward-model patches, patch b = base[b % n_distinct]
+    (a prime n_distinct keeps the sampled patches 0/128/255 distinct)."""
+    base = make_stack(Np, L, r, x0, y0, n_patch=n_distinct, seed=seed)
+    idx = np.arange(B) % n_distinct
+    return base[:, idx], idx
+
+
+def test_config3_dogstomach_literal_256_patches():
+    """Config 3 as dataset_dogStomach.json states it: 157 LEDs (maxNA 0.4) in
+    the reference's own unstable std::sort order, Np 200 / L 600 / r 26,
+    delta1 10 / delta2 3, 256 patches on one GPU, 2 iterations."""
+    import oracle_lib
+    p, x0, y0 = _probe_geometry("geometry_dogStomach_literal.json")
+    Np, L, r = p["np"], p["nlarge"], p["na_radius"]
+    assert (Np, L, r, len(x0), p["delta1"], p["delta2"]) == (200, 600, 26, 157, 10, 3)
+    order = np.arange(len(x0))
+    B = 256
+    stack, idx = _tiled_stack(Np, L, r, x0, y0, B, 7, seed=301)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=B)
+    out = fpm_amd.run_fpm(prob, stack, 2)
+    sample = (0, 128, 255)
+    assert len({int(idx[b]) for b in sample}) == 3
+    refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 2,
+                                    threads=3)
+    for i, b in enumerate(sample):
+        assert rel_l2(out["objCrop"][b], refs[i]) < 5e-5, b
+    # identical inputs give identical bits whatever the patch slot
+    np.testing.assert_array_equal(out["objCrop"][0], out["objCrop"][7])
+    np.testing.assert_array_equal(out["pupil"][128], out["pupil"][2])
+
+
+def test_config4_single_gpu_shard_128_patches():
+    """Config 4 on one GPU: the 128-patch shard one of 8 ranks owns of the
+    1024-patch field (parallel.shard_range), metric geometry (dogStomach
+    optics, maxNA 0.6: 293 LEDs, Np 256, L 768, r 33), 1 iteration."""
+    import oracle_lib
+    from fpm_amd import parallel
+    p, x0, y0 = _probe_geometry("geometry_dogStomach_metric.json")
+    Np, L, r = p["np"], p["nlarge"], p["na_radius"]
+    assert (Np, L, r, len(x0)) == (256, 768, 33, 293)
+    lo, hi = parallel.shard_range(1024, 8, 3)
+    assert hi - lo == 128
+    order = np.arange(len(x0))
+    stack, idx = _tiled_stack(Np, L, r, x0, y0, hi - lo, 5, seed=401)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=hi - lo)
+    out = fpm_amd.run_fpm(prob, stack, 1)
+    sample = (0, 63, 127)
+    assert len({int(idx[b]) for b in sample}) == 3
+    refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 1,
+                                    threads=3)
+    for i, b in enumerate(sample):
+        assert rel_l2(out["objCrop"][b], refs[i]) < 1e-5, b
 
 
 def test_config5_geometry_np1024_l4096():

@@ -59,19 +59,22 @@ def test_batched_patches_are_independent():
         assert rel_l2(out["pupil"][b], ref["pupil"]) < _tol(iters)
 
 
-def test_metric_geometry_patch_vs_cpp_oracle():
+@pytest.mark.parametrize("all_channels", [True, False], ids=["opencv_scalar", "re_only"])
+def test_metric_geometry_patch_vs_cpp_oracle(all_channels):
     """Full metric size (dogStomach optics, 293 LEDs, Np 256, L 768, r 33),
-    one iteration, against the C++ fp64 oracle run on the same box."""
+    one iteration, against the C++ fp64 oracle run on the same box, for both
+    readings of cv::add(UMat c2, double) (DESIGN.md section 2)."""
     import bench
     import oracle_lib
     geo = bench.metric_geometry()
     order = np.arange(geo["n_led"])
     stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], n_patch=1, seed=5)
     ref = oracle_lib.run_fpm(stack[:, 0], order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"],
-                             geo["d1"], geo["d2"], 1)
+                             geo["d1"], geo["d2"], 1, all_channels=all_channels)
+    flags = 0 if all_channels else fpm_amd.FLAG_SCALAR_RE_ONLY
     for path in (fpm_amd.PATH_GENERAL, fpm_amd.PATH_AUTO):
         prob = fpm_amd.Problem(geo["np_"], geo["L"], order, geo["x0"], geo["y0"], geo["r"], geo["d1"],
-                               geo["d2"], n_patch=1, path=path)
+                               geo["d2"], n_patch=1, path=path, flags=flags)
         out = fpm_amd.run_fpm(prob, stack, 1)
         assert rel_l2(out["objCrop"][0], ref["objCrop"]) < 1e-5
         assert rel_l2(out["objF"][0], ref["objF"]) < 1e-5
@@ -84,7 +87,8 @@ def test_golden_fixtures_on_gpu():
     for path in sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "solver_*.npz"))):
         g = np.load(path)
         Np, L, r, iters, d1, d2 = (int(v) for v in g["params"])
-        prob = fpm_amd.Problem(Np, L, g["order"], g["x0"], g["y0"], r, d1, d2)
+        flags = 0 if int(g["all_channels"]) else fpm_amd.FLAG_SCALAR_RE_ONLY
+        prob = fpm_amd.Problem(Np, L, g["order"], g["x0"], g["y0"], r, d1, d2, flags=flags)
         out = fpm_amd.run_fpm(prob, g["stack"], iters)
         for k in ("objF", "objCrop", "pupil"):
             assert rel_l2(out[k][0], g[k]) < _tol(iters), (path, k)

@@ -9,6 +9,9 @@ the cvComplex semantics are pinned by these known-answer tests:
         counts the survey measured on an emulation of OpenCV's fill
         (r = 26/30/33/84 -> 2121/2821/3409/22133)
 and the two independent restatements (numpy, C++) must agree to ~1e-12.
+(iv) is OpenCV's published scalar rule (cv::add / cv::multiply of a CV_64FC2
+array and a double act on every channel); test_scalar_semantics_differ shows
+the two readings give measurably different reconstructions.
 """
 import glob
 import os
@@ -50,8 +53,9 @@ def test_support_disk_pixel_counts(r, count):
 def test_oracles_reproduce_golden(path):
     g = np.load(path)
     Np, L, r, iters, d1, d2 = (int(v) for v in g["params"])
-    py = run_fpm(g["stack"], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, iters)
-    cc = oracle_lib.run_fpm(g["stack"], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, iters)
+    allc = bool(g["all_channels"])
+    py = run_fpm(g["stack"], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, iters, all_channels=allc)
+    cc = oracle_lib.run_fpm(g["stack"], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, iters, all_channels=allc)
     for k in ("objF", "objCrop", "pupil"):
         assert rel_l2(py[k], g[k]) < 1e-6, k      # fixture stored as complex64
         assert rel_l2(cc[k], py[k]) < 1e-10, k    # two fp64 restatements agree
@@ -65,3 +69,29 @@ def test_cpp_batch_equals_single():
     for b in range(2):
         one = oracle_lib.run_fpm(st[:, b], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, iters)
         assert rel_l2(batch[b], one["objCrop"]) == 0.0
+
+
+def test_scalar_semantics_differ():
+    """The complex denominators of fpmMain.cpp:417-419/469-471 (OpenCV scalar
+    unrolling) are not a rounding-level change: after one iteration the two
+    readings differ by far more than any parity tolerance."""
+    g = np.load(os.path.join(GOLDEN, "solver_np32_r6_it2.npz"))
+    Np, L, r, iters, d1, d2 = (int(v) for v in g["params"])
+    a = oracle_lib.run_fpm(g["stack"], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, 1, all_channels=True)
+    b = oracle_lib.run_fpm(g["stack"], g["order"], g["x0"], g["y0"], Np, L, r, d1, d2, 1, all_channels=False)
+    assert rel_l2(a["objCrop"], b["objCrop"]) > 1e-3
+    assert rel_l2(a["pupil"], b["pupil"]) > 1e-3
+
+
+def test_complex_denominator_restatement():
+    """One LED step of the numpy oracle against a hand-written complex division
+    (num / ((|P|^2 + d2 + i d2) max|P|)): checks the unrolled-scalar reading
+    op by op on random data."""
+    rng = np.random.default_rng(3)
+    P = rng.standard_normal((8, 8)) + 1j * rng.standard_normal((8, 8))
+    num = rng.standard_normal((8, 8)) + 1j * rng.standard_normal((8, 8))
+    d2 = 3.0
+    pa = np.abs(P)
+    den = (pa * pa + d2 + 1j * d2) * pa.max()
+    want = num * (pa * pa + d2 - 1j * d2) / (((pa * pa + d2) ** 2 + d2 * d2) * pa.max())
+    np.testing.assert_allclose(num / den, want, rtol=1e-13)
