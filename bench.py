@@ -103,18 +103,39 @@ def dense_flops_per_update(np_):
     return 2 * 5.0 * np_ * np_ * math.log2(np_ * np_) + 70.0 * np_ * np_
 
 
-def algorithmic_bytes_per_update(np_):
-    """read I (2) + read/write O ROI (8+8) + read/write P (8+8) per pixel."""
+def dense_bytes_per_update(np_):
+    """SURVEY.md 8(d) dense definition: read I (2) + read/write O ROI (8+8) +
+    read/write P (8+8) per ROI pixel = 34 Np^2.  Reported as a labelled
+    dense-equivalent figure only: the fused kernel keeps T in LDS and P in
+    registers, so these bytes never move."""
     return 34.0 * np_ * np_
 
 
-def load_pmc(path, launch_kernel):
+def min_bytes_per_update(np_, support_px, meas_bytes=2):
+    """Minimum HBM bytes one LED-update must move on the support-pruned path
+    (the headline roofline): read the measurement I (meas_bytes per pixel,
+    uint16 in the C-ABI layout) + read and write the spectrum O on the pupil
+    support (8 + 8 bytes per support pixel).  The pupil, tile maxima and
+    max|P| stay on chip for the whole launch (their per-launch bytes are
+    below 0.1 %)."""
+    return float(meas_bytes) * np_ * np_ + 16.0 * support_px
+
+
+def load_pmc(path, kernel):
+    """(per-launch HBM bytes, derived counter view, note) for `kernel` from a
+    tools/pmc_to_json.py file -- only when its src_hash matches the current
+    csrc tree, so a profile of older kernels is never reported as traffic."""
+    from tools.srchash import src_hash
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("per_launch_hbm_bytes", {}).get(launch_kernel)
-    except Exception:
-        return None
+    except Exception as e:  # noqa: BLE001
+        return None, None, f"no counter profile ({type(e).__name__})"
+    if d.get("src_hash") != src_hash():
+        return None, None, f"counter profile {os.path.basename(path)} is for csrc {d.get('src_hash')}, " \
+                           f"tree is {src_hash()}: not reported"
+    return (d.get("per_launch_hbm_bytes", {}).get(kernel), d.get("derived", {}).get(kernel),
+            f"{os.path.basename(path)} (csrc {d['src_hash']})")
 
 
 def cpu_model():
@@ -128,26 +149,69 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(geo, stack_host, threads):
+def host_cores():
+    """Cores this job may use on the host: the CPU affinity mask, capped by a
+    cgroup CPU quota when one is set (a GPU box shares its host between
+    jobs; nproc reports the whole machine).  Returns (cores, description)."""
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    cores = min(n_aff, quota) if quota else n_aff
+    return cores, f"nproc {os.cpu_count()}, affinity {n_aff}, cgroup quota {quota or 'none'}"
+
+
+def config1_geometry():
+    """BASELINE configs[0]: dataset_mono.json with the 508-LED dome fallback
+    (geometry and order from the reference's own jsoncpp probe,
+    tests/golden/geometry_mono_dome.json): Np 90, L 360, r 30, 193 LEDs."""
+    import numpy as np
+    with open(os.path.join(ROOT, "tests", "golden", "geometry_mono_dome.json")) as f:
+        p = json.load(f)["probe"]
+    leds = {l["led"]: l for l in p["leds"]}
+    order = p["sorted_indices"]
+    return dict(np_=p["np"], L=p["nlarge"], r=p["na_radius"], d1=p["delta1"], d2=p["delta2"], n_led=len(order),
+                x0=np.array([leds[n]["crop_x0"] for n in order], np.int32),
+                y0=np.array([leds[n]["crop_y0"] for n in order], np.int32))
+
+
+def cpu_baseline(geo, stack_host, threads, cores_note):
     """C++ fp64 reference-faithful restatement (oracle/liboracle.so, 'port'),
     one patch per thread, all LEDs, one iteration; wall-clock.  SURVEY.md 8(d)
     asks for the rate on all host cores (one patch per thread, patches are
-    independent) and on one core: both are measured, `value` is the former."""
+    independent), on one core, and for config 1 (dataset_mono, Np 90, 1
+    patch, 5 iterations) on one core: all three are measured, `value` is the
+    first."""
     import numpy as np
     import oracle_lib
+    from tools.synth import make_stack
     order = np.arange(geo["n_led"], dtype=np.int32)
 
-    def timed(stk, nthr):
+    def timed(stk, g, nthr, iters=1):
+        o = np.arange(g["n_led"], dtype=np.int32)
         t0 = time.perf_counter()
-        oracle_lib.run_fpm_batch(stk, order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"],
-                                 geo["d1"], geo["d2"], 1, nthr, outputs=False)
+        oracle_lib.run_fpm_batch(stk, o, g["x0"], g["y0"], g["np_"], g["L"], g["r"],
+                                 g["d1"], g["d2"], iters, nthr, outputs=False)
         return time.perf_counter() - t0
 
-    dt = timed(stack_host, threads)
-    dt1 = timed(np.ascontiguousarray(stack_host[:, :1]), 1)
+    dt = timed(stack_host, geo, threads)
+    dt1 = timed(np.ascontiguousarray(stack_host[:, :1]), geo, 1)
+    c1 = config1_geometry()
+    s1 = make_stack(c1["np_"], c1["L"], c1["r"], c1["x0"], c1["y0"], n_patch=1, seed=20261015)
+    dtc1 = timed(s1, c1, 1, iters=5)
     B = stack_host.shape[1]
+    del order
     return dict(value=round(B * geo["n_led"] / dt, 1), unit="LED-updates/s", cores=threads, kind="port",
-                single_core_value=round(geo["n_led"] / dt1, 1), cpu_model=cpu_model(),
+                single_core_value=round(geo["n_led"] / dt1, 1), cpu_model=cpu_model(), host_cores=cores_note,
+                config1_single_core=dict(value=round(5 * c1["n_led"] / dtc1, 1), unit="LED-updates/s",
+                                         seconds=round(dtc1, 2),
+                                         sample="BASELINE configs[0]: dataset_mono + dome fallback, Np 90, L 360, "
+                                                f"{c1['n_led']} LEDs, 1 patch, 5 iterations, 1 thread"),
                 sample=f"{B} patches x {geo['n_led']} LEDs x 1 iteration, Np={geo['np_']} L={geo['L']}, "
                        f"complex128, one patch per thread on {threads} threads, {dt:.1f} s wall; "
                        f"single core: 1 patch x {geo['n_led']} LEDs, {dt1:.1f} s")
@@ -164,7 +228,7 @@ def main():
                     help="workload (config_geometry); only 'metric' is the headline line")
     ap.add_argument("--fp16", action="store_true", help="fp16 spectrum storage (default for --config c5)")
     ap.add_argument("--path", default="auto", choices=["auto", "general", "fused"])
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this job may use (host_cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
@@ -215,9 +279,18 @@ def main():
                            geo["d1"], geo["d2"], n_patch=B, path=path,
                            flags=fpm_amd.FLAG_SPEC_FP16 if fp16 else 0)
     solver = fpm_amd.Solver(prob, device=local)
+    # one-time setup, reported beside the line (never in value): the device
+    # stack copy incl. the fused path's measurement permutation, and fpm_init
+    torch.cuda.synchronize()
+    s0 = time.perf_counter()
     solver.upload_device(stack.data_ptr())
     solver.synchronize()
+    s1 = time.perf_counter()
     solver.init()
+    solver.synchronize()
+    setup = dict(upload_and_permute_ms=round((s1 - s0) * 1e3, 2),
+                 init_ms=round((time.perf_counter() - s1) * 1e3, 2),
+                 note="once per reconstruction, excluded from value")
     info = solver.info()
 
     for _ in range(args.warmup):
@@ -251,25 +324,34 @@ def main():
     flops = algorithmic_flops_per_update(geo["np_"], info.box, info.support_px) * per_launch_updates
     achieved_tf = flops / (per_launch_ms * 1e-3) / 1e12
     kname = "k_fused_iteration" if info.path == fpm_amd.PATH_FUSED else "general_led_step(4 kernels)"
-    traffic = load_pmc(args.pmc, kname)
-    # Headline roofline as SURVEY.md 8(d) defines it: HBM, with the dense
-    # per-unit bytes 34 Np^2 (read I, read/write the O ROI and P).  The fused
-    # kernel executes a support-pruned, LDS-resident form of the same step, so
-    # it moves far fewer bytes (`traffic`, PMC) and beats this roof (frac > 1);
-    # its own bound is FP32 issue, reported under `compute`.
-    dense_bytes = algorithmic_bytes_per_update(geo["np_"]) * per_launch_updates
-    achieved_gbs = dense_bytes / (per_launch_ms * 1e-3) / 1e9
+    traffic, counters, pmc_note = load_pmc(args.pmc, kname)
+    # Headline roofline: HBM against the MINIMUM bytes of the support-pruned
+    # step (uint16 I + spectrum O read/write on the support, per LED-update).
+    # The kernel's binding resource is FP32 issue (`compute`); SURVEY.md
+    # 8(d)'s dense 34 Np^2 definition is kept as a labelled dense-equivalent.
+    min_bytes = min_bytes_per_update(geo["np_"], info.support_px) * per_launch_updates
+    achieved_gbs = min_bytes / (per_launch_ms * 1e-3) / 1e9
+    dense_bytes = dense_bytes_per_update(geo["np_"]) * per_launch_updates
+    dense_gbs = dense_bytes / (per_launch_ms * 1e-3) / 1e9
     roofline = dict(bound="hbm", achieved=round(achieved_gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved_gbs / HBM_PEAK_GBS, 4), traffic=traffic,
                     kernel=kname, launch_ms=round(per_launch_ms, 4),
-                    algorithmic_bytes_per_launch=dense_bytes,
+                    algorithmic_bytes_per_launch=min_bytes,
+                    bytes_model=f"2*Np^2 (uint16 I) + 16*|S| (O read+write on the {info.support_px}-px support) "
+                                f"per LED-update x {per_launch_updates} LED-updates per launch",
                     measured_hbm_GBs=(round(traffic / (per_launch_ms * 1e-3) / 1e9, 1) if traffic else None),
-                    compute=dict(peak_TFLOPs=F32_PEAK_TFLOPS,
-                                 dense_TFLOPs=round(dense_flops_per_update(geo["np_"]) * per_launch_updates
-                                                    / (per_launch_ms * 1e-3) / 1e12, 2),
+                    traffic_over_algorithmic=(round(traffic / min_bytes, 3) if traffic else None),
+                    traffic_source=pmc_note,
+                    dense_equivalent=dict(bytes_per_update=dense_bytes_per_update(geo["np_"]),
+                                          GBs=round(dense_gbs, 1), frac_of_peak=round(dense_gbs / HBM_PEAK_GBS, 4),
+                                          note="SURVEY.md 8(d) dense 34*Np^2 definition; not bytes moved"),
+                    compute=dict(bound="fp32 VALU issue", peak_TFLOPs=F32_PEAK_TFLOPS,
+                                 dense_equivalent_TFLOPs=round(dense_flops_per_update(geo["np_"]) * per_launch_updates
+                                                               / (per_launch_ms * 1e-3) / 1e12, 2),
                                  executed_TFLOPs=round(achieved_tf, 2),
                                  executed_frac=round(achieved_tf / F32_PEAK_TFLOPS, 4),
-                                 executed_flops_per_launch=flops))
+                                 executed_flops_per_launch=flops),
+                    counters=counters)
 
     gather = None
     if world > 1 and not args.no_gather:
@@ -308,9 +390,10 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "metric":
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cores, note = host_cores()
+        threads = args.cpu_threads or min(cores, B)
         host_stack = stack[:, :threads].contiguous().cpu().numpy().view(np.uint16)
-        cpu = cpu_baseline(geo, host_stack, threads)
+        cpu = cpu_baseline(geo, host_stack, threads, note)
 
     if rank == 0:
         out = {
@@ -328,6 +411,7 @@ def main():
                        "parallelism": f"patch-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "setup": setup,
             "led_ms_per_step": round(led_ms / args.steps, 3),
             "objcrop_ms_per_step": round(crop_ms / args.steps, 3),
         }

@@ -1,15 +1,25 @@
-"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes to per-launch HBM
-bytes per kernel (bench.py's roofline.traffic).
+"""Reduce rocprofv3 --pmc passes to per-launch counters per kernel
+(bench.py's roofline.traffic and roofline.counters).
 
-usage: python tools/pmc_to_json.py <pmc dir with p*/run_counter_collection.csv> <out.json>
+usage: python tools/pmc_to_json.py <pmc dir with p*/**/*counter_collection.csv> <out.json>
 
-Units and corrections (MI355X_MICROARCH.md, HBM [CDNA4]): FETCH_SIZE and
-WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of 16-B/lane
-coalesced reads and other widths are uncalibrated.  k_permute_meas reads and
-writes exactly n_img * Np^2 * 2 bytes with 2-B/lane row reads -- the access
-width of the fused kernel's measurement stream -- so its FETCH ratio is used
-as the read calibration for k_fused_iteration; k_fft_batch (8-B/lane) uses the
-guide's x2.  Raw values are kept next to the corrected ones.
+Every counter is averaged over the dispatches of one kernel (one value per
+launch).  The output is stamped with tools/srchash.py's hash of the csrc tree
+it was measured on; bench.py ignores a file whose hash differs.
+
+Units and corrections (MI355X_MICROARCH.md, HBM [CDNA4] and PMC notes):
+  * FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the
+    bytes of 16-B/lane coalesced reads; other widths are uncalibrated.
+    k_permute_meas reads exactly n_img * Np^2 * 2 bytes, so its FETCH ratio
+    calibrates the read side when it is in the same run; otherwise x2.
+  * GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = value / 8.
+  * SQ_INSTS_VALU counts wave instructions; a wave64 FP32 VALU instruction
+    occupies its SIMD for 2 cycles, so VALU issue fraction =
+    2 * SQ_INSTS_VALU / (1024 SIMDs * kernel cycles).
+  * SQ_WAVE_CYCLES, SQ_ACTIVE_INST_*, SQ_WAIT_* count quad-cycles; ratios
+    between them are unit-free.
+  * FP32 flops executed = 64 lanes * (2 FMA + ADD + MUL + TRANS) wave
+    instructions of the SQ_INSTS_VALU_*_F32 counters (when collected).
 """
 import csv
 import glob
@@ -18,46 +28,80 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from srchash import src_hash  # noqa: E402
+
+N_SIMD = 1024
+
 
 def short(name):
     for k in ("k_fused_iteration", "k_permute_meas", "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows",
-              "k_crop_cols"):
+              "k_crop_cols", "k_colpass_wave", "k_colpass_tiled", "k_gather_rowifft_tiled",
+              "k_rowfft_update_tiled", "k_tile_rows", "k_pupil_commit"):
         if k in name:
             return k
-    return name[:60]
+    return name.split("(")[0][:60]
+
+
+def derive(c):
+    d = {}
+    cyc = c.get("GRBM_GUI_ACTIVE")
+    if cyc:
+        cyc /= 8.0
+        d["kernel_cycles"] = cyc
+        if "SQ_INSTS_VALU" in c:
+            d["valu_issue_frac"] = 2.0 * c["SQ_INSTS_VALU"] / (N_SIMD * cyc)
+        f32 = [c.get(k) for k in ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                                  "SQ_INSTS_VALU_TRANS_F32")]
+        if all(v is not None for v in f32):
+            fl = 64.0 * (2 * f32[0] + f32[1] + f32[2] + f32[3])
+            d["fp32_flops"] = fl
+            d["fp32_flops_per_cycle_frac"] = fl / (N_SIMD * 64.0 * cyc)
+    wc = c.get("SQ_WAVE_CYCLES")
+    if wc:
+        for k in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY",
+                  "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS"):
+            if k in c:
+                d[k.lower().replace("sq_", "") + "_per_wave_cycle"] = c[k] / wc
+    if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c:
+        d["lds_bank_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+    return d
 
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
     acc = defaultdict(lambda: defaultdict(list))
     perm = []  # (work-items, FETCH bytes) per k_permute_meas dispatch
-    for f in glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True):
+    for f in sorted(glob.glob(os.path.join(src, "*", "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 k = short(r["Kernel_Name"])
-                acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+                v = float(r["Counter_Value"])
+                acc[k][r["Counter_Name"]].append(v)
                 if k == "k_permute_meas" and r["Counter_Name"] == "FETCH_SIZE":
-                    perm.append((int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0))
+                    perm.append((int(r["Grid_Size"]), v * 1024.0))
     raw = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
-    res = {"raw_bytes_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {}}
-    # calibration from the permutation kernel: known bytes read per launch
-    # = grid_blocks(y) * Np^2 * 2 ; its grid is (Np/64 * 256 threads) x n_img
+    res = {"src_hash": src_hash(), "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
+           "derived": {}}
     cal = None
     if perm:
-        # grid (Np/64, n_img) x 256 threads: work-items = 4 * 256 * n_img at Np 256
+        # grid (Np/64, n_img) x 256 threads at Np 256: work-items = 4 * 256 * n_img
         np_ = 256
         known = sum(g // (np_ // 64 * 256) * np_ * np_ * 2.0 for g, _ in perm)
         cal = known / sum(v for _, v in perm)
         res["permute_known_read_bytes"] = known
     for k, d in raw.items():
-        if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
-            continue
-        scale = cal if (k == "k_fused_iteration" and cal) else 2.0
-        res["read_scale"][k] = scale
-        res["per_launch_hbm_bytes"][k] = d["FETCH_SIZE"] * scale + d["WRITE_SIZE"]
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            scale = cal if (k == "k_fused_iteration" and cal) else 2.0
+            res["read_scale"][k] = scale
+            res["per_launch_hbm_bytes"][k] = d["FETCH_SIZE"] * 1024.0 * scale + d["WRITE_SIZE"] * 1024.0
+        dv = derive(d)
+        if dv:
+            res["derived"][k] = dv
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({"src_hash": res["src_hash"], "per_launch_hbm_bytes": res["per_launch_hbm_bytes"],
+                      "derived": res["derived"]}, indent=1))
 
 
 if __name__ == "__main__":

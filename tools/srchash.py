@@ -1,0 +1,30 @@
+"""Hash of the device-code sources a counter profile was measured on.
+
+bench.py only reports `roofline.traffic` (and the SQ counter view) from
+profiles/pmc_latest.json when the file's `src_hash` equals the hash of the
+current fpm-opencv_amd/csrc tree, so a stale profile is never attributed to
+changed kernels.
+
+usage: python tools/srchash.py      -> prints the hash
+"""
+import hashlib
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "fpm-opencv_amd", "csrc")
+
+
+def src_hash(csrc: str = CSRC) -> str:
+    h = hashlib.sha256()
+    for name in sorted(os.listdir(csrc)):
+        p = os.path.join(csrc, name)
+        if not os.path.isfile(p) or not name.endswith((".hip", ".hpp", ".cpp", ".h")):
+            continue
+        h.update(name.encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+if __name__ == "__main__":
+    print(src_hash())
