@@ -223,6 +223,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--patches", type=int, default=0, help="patches per GPU (0: 256, 8 for --config c5)")
+    ap.add_argument("--patches-total", type=int, default=0,
+                    help="strong scaling: one field of T patches sharded over the ranks (parallel.shard_range), "
+                         "gathered and stitched on rank 0 after the timed region; 0 = weak scaling (--patches per rank)")
     ap.add_argument("--np", type=int, default=256)
     ap.add_argument("--config", default="metric", choices=["metric", "c3", "c5"],
                     help="workload (config_geometry); only 'metric' is the headline line")
@@ -264,7 +267,18 @@ def main():
 
     geo = config_geometry(args.config, args.np)
     fp16 = args.fp16 or args.config == "c5"
-    B = args.patches if args.patches > 0 else (8 if args.config == "c5" else 256)
+    strong = args.patches_total > 0
+    if strong:
+        # strong scaling: one fixed field of T patches, contiguous shards
+        # (parallel.shard_range); data seeded per global patch
+        from fpm_amd import parallel
+        lo, hi = parallel.shard_range(args.patches_total, world, rank)
+        B, seed, poff = hi - lo, 20261015, lo
+        if B < 1:
+            raise SystemExit(f"rank {rank}: empty shard of {args.patches_total} patches over {world} ranks")
+    else:
+        B = args.patches if args.patches > 0 else (8 if args.config == "c5" else 256)
+        seed, poff = 20261015 + 1000 * rank, 0
     if args.data == "random":
         g = torch.Generator(device="cuda")
         g.manual_seed(rank)
@@ -272,7 +286,7 @@ def main():
                               dtype=torch.int32).to(torch.int16)
     else:
         stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], B,
-                           seed=20261015 + 1000 * rank, device="cuda")
+                           seed=seed, device="cuda", patch_offset=poff)
     torch.cuda.synchronize()
     path = {"auto": fpm_amd.PATH_AUTO, "general": fpm_amd.PATH_GENERAL, "fused": fpm_amd.PATH_FUSED}[args.path]
     prob = fpm_amd.Problem(geo["np_"], geo["L"], np.arange(geo["n_led"]), geo["x0"], geo["y0"], geo["r"],
@@ -317,7 +331,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    updates = B * geo["n_led"] * args.steps * world
+    updates = (args.patches_total if strong else B * world) * geo["n_led"] * args.steps
     value = updates / elapsed
     per_launch_ms = led_ms / max(launches, 1)
     per_launch_updates = B * geo["n_led"] if info.path == fpm_amd.PATH_FUSED else B
@@ -354,19 +368,33 @@ def main():
                     counters=counters)
 
     gather = None
-    if world > 1 and not args.no_gather:
+    if (world > 1 or strong) and not args.no_gather:
+        # the final exchange of SURVEY.md 8(e): every rank's objCrop tiles to
+        # rank 0 in one gather (RCCL over xGMI), then -- for a fixed field --
+        # the stitched high-resolution field on rank 0's GPU; timed beside
+        # the line, never inside value
+        from fpm_amd import parallel
         L = geo["L"]
         mine = torch.empty((B, L, L, 2), dtype=torch.float32, device="cuda")
         solver.download_objcrop_device(mine.data_ptr())
         torch.cuda.synchronize()
         mine = mine.to(cdev)
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         g0 = time.perf_counter()
-        from fpm_amd import parallel
-        parallel.gather_tiles(mine, dist, dst=0)
+        tiles = parallel.gather_tiles(mine, dist, dst=0) if world > 1 else mine
         torch.cuda.synchronize()
         gms = (time.perf_counter() - g0) * 1e3
         gather = dict(ms=round(gms, 2), GB_to_rank0=round(mine.numel() * 4 * (world - 1) / 1e9, 3))
+        if strong and rank == 0:
+            grid = parallel.field_grid(args.patches_total)
+            s0 = time.perf_counter()
+            field = parallel.stitch(tiles, grid)
+            torch.cuda.synchronize()
+            gather.update(stitch_ms=round((time.perf_counter() - s0) * 1e3, 2),
+                          field=f"{grid[0]}x{grid[1]} patches -> {field.shape[0]}x{field.shape[1]} complex64")
+            del field
+        del tiles
 
     upload = None
     if args.pcie and rank == 0:
@@ -399,13 +427,14 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "LED-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "f32 (fp16 spectrum storage)" if fp16 else "f32",
             "data": ("synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16"
                      if args.data == "model" else "random uint16 (profiling only)"),
             "config": {"workload": WORKLOADS[args.config] if args.np == 256 or args.config != "metric" else
                                    f"dogStomach optics, Np={geo['np_']}, one runFPM iteration per step",
                        "patches_per_gpu": B, "leds": int(geo["n_led"]), "np": int(geo["np_"]),
+                       **({"patches_total": args.patches_total} if strong else {}),
                        "nlarge": int(geo["L"]), "na_radius": int(geo["r"]),
                        "path": "fused" if info.path == fpm_amd.PATH_FUSED else "general",
                        "parallelism": f"patch-sharded x{world}"},

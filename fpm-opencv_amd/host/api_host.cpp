@@ -257,6 +257,36 @@ int fpm_host_load_images(fpm_host *h) {
     return (int)h->order.size();
 }
 
+int fpm_host_load_frames(const fpm_host *h, uint16_t *out, size_t n, int32_t *width, int32_t *height) {
+    if (!h) return herr(-22, "null argument");
+    if (!h->geometry_done) return herr(-71, "geometry not computed");
+    if (h->cfg.color) return herr(-22, "colour datasets (isColor) are not supported by this build");
+    int W = -1, H = -1;
+    for (size_t s = 0; s < h->order.size(); ++s) {  // fpmMain.cpp:109-121, stack order
+        const int led = h->order[s];
+        std::string name;
+        for (size_t i = 0; i < h->present.size() && i < h->names.size(); ++i)
+            if (h->present[i] == led) name = h->names[i];
+        if (name.empty()) return herr(-2, "no file for LED %d (scan the dataset first)", led);
+        Frame f;
+        std::string err;
+        if (!read_tiff(h->cfg.dataset_root + name, &f, &err)) return herr(-5, "%s", err.c_str());
+        if (s == 0) {
+            W = f.width;
+            H = f.height;
+            if (width) *width = W;
+            if (height) *height = H;
+            if (!out) return 0;
+            if (n < h->order.size() * (size_t)W * H)
+                return herr(-22, "buffer too small: %zu < %zu", n, h->order.size() * (size_t)W * H);
+        } else if (f.width != W || f.height != H) {
+            return herr(-22, "%s: frame %dx%d differs from %dx%d", name.c_str(), f.width, f.height, W, H);
+        }
+        std::memcpy(out + s * (size_t)W * H, f.px.data(), (size_t)W * H * sizeof(uint16_t));
+    }
+    return (int)h->order.size();
+}
+
 int fpm_host_get_stack(const fpm_host *h, uint16_t *out, size_t n) {
     if (!h || !out) return herr(-22, "null argument");
     if (h->stack.empty()) return herr(-71, "images not loaded");

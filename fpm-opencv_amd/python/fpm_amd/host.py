@@ -17,7 +17,7 @@ HOST_SYMBOLS = (
     "fpm_host_override", "fpm_host_set_led_table", "fpm_host_set_present", "fpm_host_scan",
     "fpm_host_geometry", "fpm_host_n_present", "fpm_host_n_used", "fpm_host_get_leds",
     "fpm_host_get_order", "fpm_host_get_crops", "fpm_host_load_images", "fpm_host_get_stack",
-    "fpm_host_read_tiff", "fpm_host_write_tiff16", "fpm_host_last_error",
+    "fpm_host_load_frames", "fpm_host_read_tiff", "fpm_host_write_tiff16", "fpm_host_last_error",
 )
 
 
@@ -72,6 +72,7 @@ def load_host_library(path: str = HOST_LIB):
         "fpm_host_get_crops": (C.c_int, [vp, i32p, i32p, C.c_int]),
         "fpm_host_load_images": (C.c_int, [vp]),
         "fpm_host_get_stack": (C.c_int, [vp, C.POINTER(C.c_uint16), C.c_size_t]),
+        "fpm_host_load_frames": (C.c_int, [vp, C.POINTER(C.c_uint16), C.c_size_t, i32p, i32p]),
         "fpm_host_read_tiff": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint16), C.c_size_t, i32p, i32p]),
         "fpm_host_write_tiff16": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint16), C.c_int32, C.c_int32]),
         "fpm_host_last_error": (C.c_char_p, []),
@@ -158,6 +159,15 @@ class Dataset:
         n = _lib.fpm_host_n_used(self._h)
         a = np.zeros((n, c.np, c.np), np.uint16)
         _chk(_lib.fpm_host_get_stack(self._h, a.ctypes.data_as(C.POINTER(C.c_uint16)), a.size))
+        return a
+
+    def frames(self) -> np.ndarray:
+        """Raw full frames of the used LEDs, uint16 [n_used][H][W], stack order."""
+        w, h = C.c_int32(), C.c_int32()
+        _chk(_lib.fpm_host_load_frames(self._h, None, 0, C.byref(w), C.byref(h)))
+        n = _lib.fpm_host_n_used(self._h)
+        a = np.zeros((n, h.value, w.value), np.uint16)
+        _chk(_lib.fpm_host_load_frames(self._h, a.ctypes.data_as(C.POINTER(C.c_uint16)), a.size, None, None))
         return a
 
 

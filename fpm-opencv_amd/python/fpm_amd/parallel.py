@@ -49,13 +49,23 @@ def gather_tiles(tiles, dist, dst: int = 0):
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
-def stitch(tiles: np.ndarray, grid: tuple[int, int]) -> np.ndarray:
+def field_grid(total: int) -> tuple[int, int]:
+    """(gy, gx) of the most nearly square grid with gy * gx == total, gy <= gx
+    (1024 patches -> 32 x 32)."""
+    gy = int(total ** 0.5)
+    while gy > 1 and total % gy:
+        gy -= 1
+    return max(gy, 1), total // max(gy, 1)
+
+
+def stitch(tiles, grid: tuple[int, int]):
     """Place tiles [P, L, L(, 2)] (row-major patch order) on a grid (gy, gx):
-    tile i lands at rows (i // gx)*L and columns (i % gx)*L."""
+    tile i lands at rows (i // gx)*L and columns (i % gx)*L.  numpy arrays
+    and torch tensors (e.g. the gathered tiles still on rank 0's GPU) alike."""
     gy, gx = grid
     P, L = tiles.shape[0], tiles.shape[1]
     if P != gy * gx:
         raise ValueError(f"{P} tiles for a {gy}x{gx} grid")
-    rest = tiles.shape[3:]
-    out = tiles.reshape((gy, gx, L, L) + rest).swapaxes(1, 2)
-    return np.ascontiguousarray(out.reshape((gy * L, gx * L) + rest))
+    rest = tuple(tiles.shape[3:])
+    out = tiles.reshape((gy, gx, L, L) + rest).swapaxes(1, 2).reshape((gy * L, gx * L) + rest)
+    return np.ascontiguousarray(out) if isinstance(out, np.ndarray) else out.contiguous()

@@ -14,6 +14,7 @@
  *   fpm_host_geometry        sin(theta), NA filter, k-space offsets (:77-168)
  *                            and the std::sort LED order (:246-258)
  *   fpm_host_load_images     imread + crop + darkfield + background (:109-144)
+ *   fpm_host_load_frames     imread only: full frames for fpm_upload_frames
  *
  * Stack convention handed to fpm_hip: stack index i holds the LED
  * sortedIndicies[i], so the processing order is 0,1,...,ledUsedCount-1.
@@ -90,6 +91,12 @@ int  fpm_host_get_crops(const fpm_host *h, int32_t *x0, int32_t *y0, int n);
 int  fpm_host_load_images(fpm_host *h);
 /* uint16 [ledUsedCount][Np][Np] in stack order. */
 int  fpm_host_get_stack(const fpm_host *h, uint16_t *out, size_t n_elems);
+
+/* Raw full frames of the used LEDs, uint16 [ledUsedCount][height][width] in
+ * stack order, for fpm_upload_frames (many patches per frame, preprocessing on
+ * the GPU).  out == NULL only reports the frame size.  Returns the frame
+ * count (0 for a size query). */
+int  fpm_host_load_frames(const fpm_host *h, uint16_t *out, size_t n_elems, int32_t *width, int32_t *height);
 
 /* 16-bit grayscale TIFF I/O (the frame format the loader reads). */
 int  fpm_host_read_tiff(const char *path, uint16_t *out, size_t cap, int32_t *width, int32_t *height);

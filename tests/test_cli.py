@@ -38,6 +38,71 @@ def test_use_cpu_sh_device_is_refused(tmp_path):
     assert "MI355X" in r.stderr
 
 
+@pytest.mark.parametrize("value", ["CPU:0", ":CPU:0", "AMD Accelerated Parallel Processing:CPU:1", "cpu", ":GPU|CPU:0"])
+def test_opencl_cpu_selections_are_refused(tmp_path, value):
+    ds = make_dataset(str(tmp_path))
+    r = _run([ds["json"], "1"], env={"OPENCV_OPENCL_DEVICE": value})
+    assert r.returncode == 3, (value, r.stdout, r.stderr)
+
+
+@pytest.mark.parametrize("value,extra,ordinal", [
+    ("GPU:0", [], 0),                 # use_gpu.sh as shipped
+    ("GPU:1", [], 1),
+    (":GPU:2", [], 2),                # OpenCV's <platform>:<type>:<device>
+    ("AMD:GPU:3", [], 3),
+    (":GPU:", [], 0),
+    ("GPU:1", ["--device", "4"], 4),  # --device wins
+])
+def test_opencl_gpu_index_selects_ordinal(tmp_path, value, extra, ordinal):
+    # no dataset directory: the run stops at the loader, after the device line
+    r = _run([str(tmp_path / "missing.json"), "1"] + extra, env={"OPENCV_OPENCL_DEVICE": value})
+    assert f"Device: MI355X ordinal {ordinal}" in r.stdout.splitlines(), (value, r.stdout)
+    assert r.returncode == 1
+
+
+def test_grid_option_is_validated(tmp_path):
+    r = _run([str(tmp_path / "missing.json"), "1", "--grid", "0x3"])
+    assert r.returncode == 2 and "GXxGY" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_grid_stitched_field_matches_oracle(tmp_path):
+    """fpmMain --grid 2x2: four patches cut on the GPU from every full frame
+    (fpm_upload_frames), solved in one batch, stitched into one field.  Each
+    tile must match the host front-end's single-crop load at that patch's
+    cropX/cropY run through the oracle."""
+    from fpm_amd import host
+    from fpm_oracle import rel_l2, run_fpm
+    ds = make_dataset(str(tmp_path / "data"))
+    out = tmp_path / "out"
+    out.mkdir()
+    r = _run([ds["json"], "2", "--out", str(out), "--grid", "2x2"], env={"OPENCV_OPENCL_DEVICE": "GPU:0"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    meta = json.loads((out / "result.json").read_text())
+    assert meta["grid"]["patches"] == 4 and meta["device"] == 0
+    field = np.load(out / "objCrop_field.npy")
+    pupils = np.load(out / "pupils.npy")
+    k = ds["keys"]
+    L = meta["nlarge"]
+    Np = meta["np"]
+    assert field.shape == (2 * L, 2 * L) and field.dtype == np.complex64
+    assert pupils.shape == (4, Np, Np)
+    for b in range(4):
+        i, j = divmod(b, 2)
+        d = host.Dataset(ds["json"])
+        d.override("cropX", k["cropX"] + j * Np)
+        d.override("cropY", k["cropY"] + i * Np)
+        d.scan()
+        n = d.geometry()
+        d.load_images()
+        cfg = d.config()
+        x0, y0 = d.crops()
+        ref = run_fpm(d.stack(), np.arange(n), x0, y0, cfg.np, cfg.nlarge, cfg.na_radius, cfg.delta1, cfg.delta2, 2)
+        tile = field[i * L:(i + 1) * L, j * L:(j + 1) * L]
+        assert rel_l2(tile, ref["objCrop"]) < 5e-5, b
+        assert rel_l2(pupils[b], ref["pupil"]) < 5e-5, b
+
+
 @pytest.mark.gpu
 def test_cli_end_to_end_matches_oracle(tmp_path):
     from fpm_amd import host

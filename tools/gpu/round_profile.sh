@@ -19,17 +19,25 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "PROF rc=$?"; tail $O/prof.log; exit 1; }
 python3 tools/prof_summary.py $O/prof $O/kernel_stats.csv
+python3 tools/prof_summary.py $O/prof $O/kernel_stats_fpm.csv "fpm::" > /dev/null
+rm -rf $O/prof   # full traces of the synthetic-input torch kernels exceed gpurun's 64 MiB copy-back
 KRE=${KRE:-"k_fused|k_permute|k_crop"}
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
-         "SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
-         "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
+         "SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex "$KRE" --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc/p$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_p$i.log 2>&1 || { echo "PMC pass $i rc=$?"; tail -5 $O/pmc_p$i.log; exit 1; }
   echo "pmc pass $i done"
 done
+# FP32 instruction mix (only when this rocprofv3 lists the counters)
+rocprofv3 -L > $O/counters_list.txt 2>&1 || true
+if grep -q SQ_INSTS_VALU_FMA_F32 $O/counters_list.txt; then
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "$KRE" --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc/p9 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_p9.log 2>&1 || { echo "PMC pass 9 rc=$?"; tail -5 $O/pmc_p9.log; exit 1; }
+  echo "pmc pass 9 done"
+fi
 python3 tools/pmc_to_json.py $O/pmc $O/pmc_latest.json > $O/pmc_summary.txt || { echo "pmc_to_json failed"; exit 1; }
 cat $O/pmc_summary.txt
+find $O/pmc -name '*kernel_trace.csv' -delete
 timeout -k 10 600 python bench.py --pmc $O/pmc_latest.json > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED rc=$?"; tail $O/bench.err; exit 1; }
 cat $O/bench.json
