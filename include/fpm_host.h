@@ -93,8 +93,8 @@ int  fpm_host_load_images(fpm_host *h);
 int  fpm_host_get_stack(const fpm_host *h, uint16_t *out, size_t n_elems);
 
 /* Raw full frames of the used LEDs, uint16 [ledUsedCount][height][width] in
- * stack order, for fpm_upload_frames (many patches per frame, preprocessing on
- * the GPU).  out == NULL only reports the frame size.  Returns the frame
+ * stack order, input of fpm_upload_frames: many patches per frame, preprocessing on
+ * the GPU.  out == NULL only reports the frame size.  Returns the frame
  * count (0 for a size query). */
 int  fpm_host_load_frames(const fpm_host *h, uint16_t *out, size_t n_elems, int32_t *width, int32_t *height);
 
