@@ -30,11 +30,12 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
                           hipStream_t s);
 // fused path (fpm_fused.hip)
-bool fused_supported(int np, int r, int L);
+int fused_threads(int np, int r, int L, const DevState &st);
+size_t fused_park_elems(int nt, int B);
 hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s);
 hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  unsigned long long *dbg, hipStream_t s);
+                                  float2 *pscr, int nt, unsigned long long *dbg, hipStream_t s);
 size_t fused_meas_bytes(int np, int B, int n_stack);
 hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
                                    const int *py0_dev, int bk1x, int bk1y, int bk2x, int bk2y, double bg_threshold,
@@ -105,6 +106,8 @@ struct fpm_ctx {
     float2 *objcrop = nullptr;
     uint16_t *meas = nullptr;
     float *meas_perm = nullptr;     // fused-path layout (reciprocal intensities)
+    float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
+    int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -286,11 +289,12 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         }
 
     const bool fp16 = (prob->flags & FPM_FLAG_SPEC_FP16) != 0;
-    if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_supported(np, r, L)))
+    c->fused_nt = fused_threads(np, r, L, st);
+    if (prob->path == FPM_PATH_FUSED && (fp16 || !c->fused_nt))
         return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
                             fp16 ? " with fp16 spectrum storage" : ""));
     c->path = (prob->path == FPM_PATH_GENERAL || fp16) ? FPM_PATH_GENERAL
-              : fused_supported(np, r, L)              ? FPM_PATH_FUSED
+              : c->fused_nt                            ? FPM_PATH_FUSED
                                                        : FPM_PATH_GENERAL;
     // fp16 storage scale: 2^-ceil(log2 Np^2) (fpm_state.hpp)
     int e2 = 0;
@@ -323,6 +327,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(float))))
             return fail(rc);
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
+        if ((rc = dalloc(c, &c->pscr, fused_park_elems(c->fused_nt, B)))) return fail(rc);
     }
     st.meas = c->meas;
     st.disk = c->disk_dev;
@@ -507,7 +512,8 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
         if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
-                                           c->prob.n_order, c->tw_np, c->dbg, c->stream));
+                                           c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->dbg,
+                                           c->stream));
         } else if (use_graph) {
             HIP_TRY(hipGraphLaunch(c->led_graph_exec, c->stream));
         } else {

@@ -44,10 +44,7 @@ namespace fpm {
 
 namespace fz {
 constexpr int NP = 256;
-constexpr int NT = 512;            // 8 waves: 2 per SIMD, 256-VGPR budget
-constexpr int NG = NT / 16;         // 32 groups of 16 lanes
-constexpr int NROWS = 64;           // FFT rows per patch (2 per group)
-constexpr int RPG = NROWS / NG;     // rows per group
+constexpr int NROWS = 64;           // FFT rows per patch (RPG = NROWS / groups per group)
 constexpr int MAXTAIL = 64;         // tail pixels (one owner thread each)
 constexpr int MAXTAILROWS = 8;
 constexpr int SK[6] = {0, 1, 2, 13, 14, 15};  // registers that can hold |kx| <= 47
@@ -59,6 +56,8 @@ struct FusedArgs {
     const float *meas_perm;     // [nS][B][x][t][m2]: 1/I[t + 16 m2][x] (+inf where I = 0)
     const int *order, *x0, *y0;
     const float2 *tw;           // exp(-2 pi i k / 256), k < 256
+    float2 *pscr;               // 1024-thread variant: lane-private parking of P and F
+                                // [B][2][6][NT] (registers freed across pass B)
     int n_order;
     int ky_lo, n_fft_rows;      // FFT rows ky_lo .. ky_lo + n_fft_rows - 1 (sigma 0..)
     int n_tail_rows;
@@ -67,9 +66,10 @@ struct FusedArgs {
     int2 tail_px[fz::MAXTAIL];  // (ky, kx), sorted by row then kx
     // tail row q holds pixels tail_px[p0 .. p0+np) with kx = kx0, kx0+1, ...
     int tail_row_p0[fz::MAXTAILROWS], tail_row_np[fz::MAXTAILROWS], tail_row_kx0[fz::MAXTAILROWS];
-    int ntiles, nwords;         // tiles of |spec| maxima, 32-bit words of the dirty bitmap
     // tiles of the spectrum's live band (fpm_state.hpp): every other tile is
-    // exactly 0 and never dirty, so max|objF| only scans these nbt tiles
+    // exactly 0 and never changes, so the kernel keeps maxima and dirty bits
+    // for these nbt tiles only (band tile k = (bty0 + k / nbx, btx0 + k % nbx));
+    // st.tdirty holds the band-indexed bits between launches
     int btx0, bty0, nbx, nbt;
     float rnbx;                 // 1 / nbx
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
@@ -131,27 +131,6 @@ __device__ __forceinline__ void dft16_out6(float2 (&v)[16], float2 (&o)[6]) {
     o[5] = y3(v[12], v[13], v[14], v[15]);             // m = 15
 }
 
-// inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six
-// SK registers may be non-zero), output r[m2] = x[t + 16 m2]
-__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const float2 (&wt)[16], int t, int xrd) {
-    float2 y[16];
-    dft16_in6<true>(v, y);
-#pragma unroll
-    for (int m1 = 1; m1 < 16; ++m1) y[m1] = cmul(y[m1], cconj(wt[m1]));
-    exchange16(scr, t, xrd, y, v);
-    dft16<true>(v, r);
-}
-
-// forward 256-point DFT, input v[n2] = x[t + 16 n2], output o[s] = X[t + 16 SK[s]]
-__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const float2 (&wt)[16], int t, int xrd) {
-    float2 y[16];
-    dft16<false>(v, y);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
-    exchange16(scr, t, xrd, y, v);
-    dft16_out6<false>(v, o);
-}
-
 // 16-point DFT whose input is zero outside v[8H .. 8H+7] (one half of a row)
 template <bool INV, int H>
 __device__ __forceinline__ void dft16_inhalf(float2 (&v)[16], float2 (&r)[16]) {
@@ -178,16 +157,100 @@ __device__ __forceinline__ void dft16_inhalf(float2 (&v)[16], float2 (&r)[16]) {
     for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
 }
 
+// Exchange of the four-step transforms.  NT = 512: the full 16 x 16 tile per
+// group (dft16.hpp exchange16).  NT = 1024: 64 groups' full tiles (147 KB)
+// do not fit beside the half-T, so each group owns HALF a tile (8 rows, 73.7 KB
+// for all groups) and exchanges in two rounds: every lane writes y[0..7],
+// lanes t < 8 read their row; every lane writes y[8..15], lanes t >= 8 read.
+// The second round's writes may not overtake the first round's reads: LDS
+// operations of one wave execute in issue order, and the laundered read base
+// keeps the compiler from reordering them (see exchange16).
+template <bool HALF>
+__device__ __forceinline__ void xchg(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
+    if constexpr (!HALF) {
+        exchange16(scr, t, xrd, y, z);
+    } else {
+        const float4 *rp = (const float4 *)(scr + xrd);  // row (t & 7), 16-B aligned (XP even)
+#pragma unroll
+        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[m1];
+        if (t < 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 q = rp[j];
+                z[2 * j] = make_float2(q.x, q.y);
+                z[2 * j + 1] = make_float2(q.z, q.w);
+            }
+        }
+#pragma unroll
+        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[8 + m1];
+        if (t >= 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 q = rp[j];
+                z[2 * j] = make_float2(q.x, q.y);
+                z[2 * j + 1] = make_float2(q.z, q.w);
+            }
+        }
+    }
+}
+
+// Four-step twiddles W256^{m t} (m = 0..15) of lane t: held in 32 VGPRs for a
+// whole half (REG, NT = 512: a table read per use serialised on LDS latency at
+// two waves per SIMD) or read from the LDS table tw2[m][t] at each use (NT =
+// 1024: four waves per SIMD hide the latency, and the registers are needed).
+template <bool REG>
+struct Tw;
+template <>
+struct Tw<true> {
+    float2 w[16];
+    __device__ __forceinline__ void load(const float2 *tw2, int t) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) w[m] = tw2[m * 16 + t];
+    }
+    __device__ __forceinline__ float2 operator[](int m) const { return w[m]; }
+};
+template <>
+struct Tw<false> {
+    const float2 *p;
+    __device__ __forceinline__ void load(const float2 *tw2, int t) { p = tw2 + t; }
+    __device__ __forceinline__ float2 operator[](int m) const { return p[m * 16]; }
+};
+
+// inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six
+// SK registers may be non-zero), output r[m2] = x[t + 16 m2]
+template <bool HALF, class TW>
+__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const TW &wt, int t,
+                                            int xrd) {
+    float2 y[16];
+    dft16_in6<true>(v, y);
+#pragma unroll
+    for (int m1 = 1; m1 < 16; ++m1) y[m1] = cmul(y[m1], cconj(wt[m1]));
+    xchg<HALF>(scr, t, xrd, y, v);
+    dft16<true>(v, r);
+}
+
+// forward 256-point DFT, input v[n2] = x[t + 16 n2], output o[s] = X[t + 16 SK[s]]
+template <bool HALF, class TW>
+__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt, int t,
+                                            int xrd) {
+    float2 y[16];
+    dft16<false>(v, y);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
+    xchg<HALF>(scr, t, xrd, y, v);
+    dft16_out6<false>(v, o);
+}
+
 // forward 256-point DFT of a half row (x = t + 16 n2, n2 in [8H, 8H+8), zero
 // elsewhere), output o[s] = X[t + 16 SK[s]]
-template <int H>
-__device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr,
-                                                   const float2 (&wt)[16], int t, int xrd) {
+template <bool HALF, int H, class TW>
+__device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt, int t,
+                                                   int xrd) {
     float2 y[16];
     dft16_inhalf<false, H>(v, y);
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
-    exchange16(scr, t, xrd, y, v);
+    xchg<HALF>(scr, t, xrd, y, v);
     dft16_out6<false>(v, o);
 }
 
@@ -206,30 +269,54 @@ __device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s]
 constexpr int TH = fz::NP / 2;
 constexpr int TLD = TH + 1;
 
-__global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
+// Kernel configurations:
+//   NT = 512  : 32 groups, 2 FFT rows each, 2 waves per SIMD (256 VGPRs), full
+//               exchange tiles, measurement and T slots prefetched one pass-B
+//               column ahead, P and F in registers throughout.
+//   NT = 1024 : 64 groups, 1 FFT row each, 4 waves per SIMD (128 VGPRs), half
+//               exchange tiles (xchg), no prefetch (the other waves of the
+//               SIMD hide the latency), and P / F parked in a lane-private
+//               global scratch while pass B runs so they hold no registers.
+template <int NT>
+struct FzCfg {
+    static constexpr int NG = NT / 16;            // 16-lane groups
+    static constexpr int RPG = fz::NROWS / NG;    // FFT rows per group
+    static constexpr int NW = NT / 64;            // waves
+    static constexpr bool HALF = NT > 512;        // half exchange tiles
+    static constexpr bool PARK = NT > 512;        // P / F parked across pass B
+    static constexpr int XT = HALF ? 8 * XP : XTILE;  // exchange tile per group (complex)
+};
+
+template <int NT>
+__global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     using namespace fz;
+    using C = FzCfg<NT>;
+    constexpr int NG = C::NG, RPG = C::RPG, NW = C::NW;
+    constexpr bool HALF = C::HALF, PARK = C::PARK;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
-    float2 *scr_all = sm;                           // NG * XTILE: per-group exchange tiles
-    float2 *th = scr_all + NG * XTILE;              // (nrows + 2) * TLD: half of T = row IDFTs of the box rows
-    float2 *tw2 = th + (nrows + 2) * TLD;           // [m1][t] = W256^{m1 t}  (after the zero + dummy rows)
+    float2 *scr_all = sm;                           // NG * XT: per-group exchange tiles
+    float2 *th = scr_all + NG * C::XT;              // (nrows + 2) * TLD: half of T = row IDFTs of the box rows
+    float2 *tw2 = th + (nrows + 2) * TLD;           // [m][t] = W256^{m t}  (after the zero + dummy rows)
     float2 *tw = tw2 + 256;                         // W256^k
     float2 *tailX = tw + 256;                       // MAXTAIL
     float2 *tailF = tailX + MAXTAIL;                // MAXTAIL
-    float *red = (float *)(tailF + MAXTAIL);        // 32
-    int *sig = (int *)(red + 32);                   // 96: T row of ky in [-48, 47], -1 outside the box
+    float *red = (float *)(tailF + MAXTAIL);        // 48: clean / dirty / pupil maxima per wave
+    int *sig = (int *)(red + 48);                   // 96: T row of ky in [-48, 47], -1 outside the box
     int2 *tpx = (int2 *)(sig + 96);                 // MAXTAIL tail pixels (ky, kx)
     int *tky = (int *)(tpx + MAXTAIL);              // MAXTAILROWS tail rows
-    float *tmx = (float *)(tky + MAXTAILROWS);      // ntiles: max|spec| per 16x16 tile (upper bound if dirty)
-    unsigned *dirty = (unsigned *)(tmx + a.ntiles); // ntiles bits: tile max may be stale-high
+    float *tmx = (float *)(tky + MAXTAILROWS);      // nbt: max|spec| per band tile (upper bound if dirty)
+    unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits: tile max may be stale-high
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
-    const int xrd = exch_rbase(t);  // exchange read base, see exchange16
+    // exchange read base (see exchange16 / xchg)
+    const int xrd = HALF ? opaque_int((t & 7) * XP) : exch_rbase(t);
     const int lane = tid & 63, w = tid >> 6;
     const int b = blockIdx.x;
     const int R = st.r, NB = st.nb, L = st.L;
-    float2 *scr = scr_all + g * XTILE;
+    float2 *scr = scr_all + g * C::XT;
+    const int nwords = (a.nbt + 31) >> 5;
 
     // ---- one-time setup (kernel-argument tables indexed with uniform indices only)
     if (tid == 0) {
@@ -253,13 +340,27 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         }
         sig[i] = s;
     }
-    float *tmax_g = st.tmax + (size_t)b * a.ntiles;
-    unsigned *dirty_g = st.tdirty + (size_t)b * a.nwords;
-    for (int i = tid; i < a.ntiles; i += NT) tmx[i] = tmax_g[i];
-    for (int i = tid; i < a.nwords; i += NT) dirty[i] = dirty_g[i];
+    // band tiles k <-> global tile (bty0 + k / nbx, btx0 + k % nbx); (k + 0.5) / nbx
+    // is never within float rounding of an integer for k < 2^16
+    auto band_dy = [&](int k) { return (int)(((float)k + 0.5f) * a.rnbx); };
+    auto band_gtile = [&](int k) {
+        const int dy = band_dy(k);
+        return (a.bty0 + dy) * st.ntx + a.btx0 + (k - dy * a.nbx);
+    };
+    float *tmax_g = st.tmax + (size_t)b * st.ntx * st.nty;
+    unsigned *dirty_g = st.tdirty + (size_t)b * ((st.ntx * st.nty + 31) / 32);
+    for (int k = tid; k < a.nbt; k += NT) tmx[k] = tmax_g[band_gtile(k)];
+    for (int i = tid; i < nwords; i += NT) dirty[i] = dirty_g[i];
 
     float2 *spec = st.spec + (size_t)b * L * L;
     float2 *pup = st.pupil + (size_t)b * NB * NB;
+    // parking slots of this lane, wave-major [b][w][P 6*RPG | F 6*RPG][64 lanes]:
+    // coalesced 512-B wave accesses, and every slot an immediate offset from
+    // one of two per-lane bases
+    float2 *parkp = a.pscr + ((size_t)(b * NW + w) * 12 * RPG) * 64 + lane;
+    float2 *parkf = parkp + 6 * RPG * 64;
+    auto parkP = [&](int j, int s) -> float2 & { return parkp[(j * 6 + s) * 64]; };
+    auto parkF = [&](int j, int s) -> float2 & { return parkf[(j * 6 + s) * 64]; };
     int kyr[RPG];
     bool ron[RPG];
     float2 P[RPG][6];
@@ -275,8 +376,17 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             const bool in = ron[j] && (kyr[j] * kyr[j] + kx * kx <= R * R);
             inmask[j] |= (in ? 1u : 0u) << s;
             P[j][s] = in ? pup[(kyr[j] + R) * NB + kx + R] : make_float2(0.f, 0.f);
+            if (PARK) parkP(j, s) = P[j][s];
         }
     }
+    auto loadP = [&]() {
+        if (PARK) {
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) P[j][s] = parkP(j, s);
+        }
+    };
     __syncthreads();  // tpx / tky / sig
     // per-lane half-T row offsets of this lane's six column slots; rows
     // outside the box read the zero row `nrows` and write the dummy row after it
@@ -314,8 +424,12 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         const int ln = a.order[itn];
         return spec + (unsigned)((a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2);
     };
+    // slot s of row j sits at a compile-time offset from the lane's row base
+    // (kx = t + 16 SK[s] - Np [s >= 3]), so one base register serves all six
+    auto soff = [](int s) { return 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); };
     auto ldO = [&](const float2 *sr, int j, int s) {
-        return ((inmask[j] >> s) & 1) ? sr[kyr[j] * L + slot_kx(t, s)] : make_float2(0.f, 0.f);
+        const float2 *lr = sr + (kyr[j] * L + t);
+        return ((inmask[j] >> s) & 1) ? lr[soff(s)] : make_float2(0.f, 0.f);
     };
     float2 Opre[RPG][6];
     if (a.n_order > 0) {
@@ -342,25 +456,23 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         float2 F[RPG][6];  // row-DFT outputs; complete after the second half
 #pragma unroll 1
         for (int h = 0; h < 2; ++h) {
-            // this lane's four-step twiddles W256^{m t}, m = 0..15, in registers
-            // for the whole half (a table read per use serialises on LDS latency)
-            float2 wt[16];
+            // this lane's four-step twiddles W256^{m t}, m = 0..15 (Tw)
+            Tw<!PARK> wt;
+            wt.load(tw2, t);
+            // measurement I[t + 16 m2][x] for this lane's pass-B columns; NT
+            // 512 issues the first column before pass A and prefetches one
+            // round ahead inside pass B, NT 1024 loads at the top of each round
+            constexpr int NQ = TH / (4 * NW);
+            auto colx = [&](int q) { const int r8 = w + NW * q; return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
+            auto ldI = [&](int q, uint4 (&n)[4]) {
+                const uint4 *ip = (const uint4 *)(Ib + ((colx(q) + TH * h) * 16 + t) * 16);
 #pragma unroll
-            for (int m = 0; m < 16; ++m) wt[m] = tw2[m * 16 + t];
-            // measurement I[t + 16 m2][x] for this lane's first pass-B column,
-            // issued before pass A so the HBM latency hides behind it; later
-            // columns are prefetched one round ahead inside pass B
-            constexpr int NQ = TH / (4 * (NT / 64));
-            auto colx = [&](int q) { const int r8 = w + (NT / 64) * q; return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
-            uint4 n0, n1, n2, n3;
-            {
-                const uint4 *ip = (const uint4 *)(Ib + ((colx(0) + TH * h) * 16 + t) * 16);
-                n0 = ld_stream(ip);
-                n1 = ld_stream(ip + 1);
-                n2 = ld_stream(ip + 2);
-                n3 = ld_stream(ip + 3);
-            }
+                for (int i = 0; i < 4; ++i) n[i] = ld_stream(ip + i);
+            };
+            uint4 nI[4];
+            if (!PARK) ldI(0, nI);
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
+            loadP();
             float2 X[RPG][6];
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
@@ -373,7 +485,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = X[j][s];
-                idft256_in6(v, r, scr, wt, t, xrd);
+                idft256_in6<HALF>(v, r, scr, wt, t, xrd);
                 float2 *row = th + (g + NG * j) * TLD + t;
                 if (h == 0) {
 #pragma unroll
@@ -411,35 +523,38 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             FPM_STAMP(1)
 
             // ---- B: columns x in [128h, 128h+128): IDFT, amplitude replacement, DFT (:365-394)
-            // the column's six half-T slots are read one round ahead as well
             float2 tin[6];
+            if (!PARK) {  // the column's six half-T slots, read one round ahead
 #pragma unroll
-            for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(0)];
+                for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(0)];
+            }
 #pragma unroll 1
             for (int q = 0; q < NQ; ++q) {
                 const int xl = colx(q);
-                const uint4 i0 = n0, i1 = n1, i2 = n2, i3 = n3;
-                {   // unconditional (the last round re-reads its own column) so
+                uint4 cI[4];
+                if (PARK) {
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xl];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cI[i] = nI[i];
+                    // unconditional (the last round re-reads its own column) so
                     // the load is not sunk into a branch at the loop latch
-                    const int qn = q + 1 < NQ ? q + 1 : q;
-                    const uint4 *ip = (const uint4 *)(Ib + ((colx(qn) + TH * h) * 16 + t) * 16);
-                    n0 = ld_stream(ip);
-                    n1 = ld_stream(ip + 1);
-                    n2 = ld_stream(ip + 2);
-                    n3 = ld_stream(ip + 3);
+                    ldI(q + 1 < NQ ? q + 1 : q, nI);
                 }
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = tin[s];
-                idft256_in6(v, r, scr, wt, t, xrd);
-                {
+                if (PARK) ldI(q, cI);  // FPM_JIT_MEAS experiment: after the inverse transform
+                idft256_in6<HALF>(v, r, scr, wt, t, xrd);
+                if (!PARK) {
                     const int xn = colx(q + 1 < NQ ? q + 1 : q);
 #pragma unroll
                     for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
                 }
-                const unsigned iw[16] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w,
-                                         i2.x, i2.y, i2.z, i2.w, i3.x, i3.y, i3.z, i3.w};
+                const unsigned iw[16] = {cI[0].x, cI[0].y, cI[0].z, cI[0].w, cI[1].x, cI[1].y, cI[1].z, cI[1].w,
+                                         cI[2].x, cI[2].y, cI[2].z, cI[2].w, cI[3].x, cI[3].y, cI[3].z, cI[3].w};
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
                     const float invI = __uint_as_float(iw[m2]);
@@ -451,7 +566,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                     v[m2] = make_float2(r[m2].x * sc, r[m2].y * sc);
                 }
                 float2 o[6];
-                dft256_out6(v, o, scr, wt, t, xrd);
+                dft256_out6<HALF>(v, o, scr, wt, t, xrd);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
             }
@@ -459,14 +574,10 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
             FPM_STAMP(2)
 
             // ---- C: this half's share of the pruned row DFTs (:394)
-            float2 Fp[RPG][6];
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    Opre[j][s] = ldO(srow, j, s);
-                    Fp[j][s] = h ? F[j][s] : make_float2(0.f, 0.f);
-                }
+                for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(srow, j, s);
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
                 if (!ron[j]) {
@@ -481,16 +592,22 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 if (h == 0) {
 #pragma unroll
                     for (int m = 0; m < 8; ++m) v[m] = row[16 * m];
-                    dft256_inhalf_out6<0>(v, o, scr, wt, t, xrd);
+                    dft256_inhalf_out6<HALF, 0>(v, o, scr, wt, t, xrd);
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) F[j][s] = o[s];
                 } else {
 #pragma unroll
                     for (int m = 0; m < 8; ++m) v[8 + m] = row[16 * m];
-                    dft256_inhalf_out6<1>(v, o, scr, wt, t, xrd);
-                }
+                    dft256_inhalf_out6<HALF, 1>(v, o, scr, wt, t, xrd);
 #pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    F[j][s] = cadd(Fp[j][s], o[s]);
+                    for (int s = 0; s < 6; ++s) F[j][s] = cadd(PARK ? parkF(j, s) : F[j][s], o[s]);
                 }
+            }
+            if (PARK && h == 0) {  // F is not held through the second half's passes A and B
+#pragma unroll
+                for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) parkF(j, s) = F[j][s];
             }
             FPM_STAMP(8)
             for (int pp = g; pp < a.n_tail_px; pp += NG) {  // tail pixels: 16 lanes sum 128 terms
@@ -527,11 +644,12 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         // needed (64 lanes of a wave hit 2-4 tile words, and an unfiltered
         // LDS atomic serialises them: 3.7k cycles per LED).
         auto note = [&](int py, int px, float ao, float an) {
-            const int ti = (py >> 4) * st.ntx + (px >> 4);
+            const int ti = ((py >> 4) - a.bty0) * a.nbx + ((px >> 4) - a.btx0);  // band tile
             const unsigned cur = tmu[ti];
             if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
+        loadP();
         // Straight-line over all slots: outside the support O = P = 0, so the
         // numerator is exactly 0 and only the spectrum store and the tile
         // bookkeeping need the mask.
@@ -552,7 +670,7 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 // this group's own half-T row is no longer read: park the numerator there
                 th[(g + NG * j) * TLD + s * 16 + t] = cmul(cmul(D, cscale(cconj(o), oa)), kip);
                 if ((inmask[j] >> s) & 1) {
-                    srow[kyr[j] * L + kx] = nv;
+                    (srow + (kyr[j] * L + t))[soff(s)] = nv;
                     note(yc + kyr[j], xc + kx, oa, cmag(nv));
                 }
             }
@@ -582,19 +700,11 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
 
         // ---- exact max|objF| (:460,467): max over clean tiles; dirty tiles
         // only matter (and are re-read) when their bound exceeds that max
-        // band tile k -> tile (ty, tx); (k + 0.5) / nbx is never within float
-        // rounding of an integer for k < 2^16
-        auto band_ty = [&](int k) { return a.bty0 + (int)(((float)k + 0.5f) * a.rnbx); };
-        auto band_tile = [&](int k) {
-            const int dy = (int)(((float)k + 0.5f) * a.rnbx);
-            return (a.bty0 + dy) * st.ntx + a.btx0 + (k - dy * a.nbx);
-        };
         float cm = 0.f, dm = 0.f;
         for (int k = tid; k < a.nbt; k += NT) {
-            const int i = band_tile(k);
-            const bool d = (dirty[i >> 5] >> (i & 31)) & 1u;
-            if (d) dm = fmaxf(dm, tmx[i]);
-            else cm = fmaxf(cm, tmx[i]);
+            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
+            if (d) dm = fmaxf(dm, tmx[k]);
+            else cm = fmaxf(cm, tmx[k]);
         }
         cm = wave_max(cm);
         dm = wave_max(dm);
@@ -606,16 +716,15 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         cm = red[0];
         dm = red[16];
 #pragma unroll
-        for (int i = 1; i < NT / 64; ++i) {
+        for (int i = 1; i < NW; ++i) {
             cm = fmaxf(cm, red[i]);
             dm = fmaxf(dm, red[16 + i]);
         }
         float omax = cm;
         if (dm > cm) {  // block-uniform: rare (bright-field LEDs, first LED of an iteration)
-            for (int k = w; k < a.nbt; k += NT / 64) {
-                const int i = band_tile(k);
-                if (!((dirty[i >> 5] >> (i & 31)) & 1u) || !(tmx[i] > cm)) continue;  // wave-uniform
-                const int ty = band_ty(k), tx = i - ty * st.ntx;
+            for (int k = w; k < a.nbt; k += NW) {
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;  // wave-uniform
+                const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
                 float mm = 0.f;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
@@ -624,23 +733,21 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 }
                 mm = wave_max(mm);
                 if (lane == 0) {
-                    tmx[i] = mm;
-                    atomicAnd(&dirty[i >> 5], ~(1u << (i & 31)));
+                    tmx[k] = mm;
+                    atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
                 }
             }
             __syncthreads();
             float m2 = 0.f;
-            for (int k = tid; k < a.nbt; k += NT) {
-                const int i = band_tile(k);
-                if (!((dirty[i >> 5] >> (i & 31)) & 1u)) m2 = fmaxf(m2, tmx[i]);
-            }
+            for (int k = tid; k < a.nbt; k += NT)
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
             m2 = wave_max(m2);
             __syncthreads();  // red[] reads above are done
             if (lane == 0) red[w] = m2;
             __syncthreads();
             omax = red[0];
 #pragma unroll
-            for (int i = 1; i < NT / 64; ++i) omax = fmaxf(omax, red[i]);
+            for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
         }
         FPM_STAMP(5)
         const float rom = 1.0f / omax;
@@ -653,21 +760,22 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
                 const float2 n = th[(g + NG * j) * TLD + s * 16 + t];
                 P[j][s] = make_float2(P[j][s].x + n.x * rom, P[j][s].y + n.y * rom);
                 pmx = fmaxf(pmx, cabs2(P[j][s]));
+                if (PARK) parkP(j, s) = P[j][s];
             }
         if (towner) {
             Pt = make_float2(Pt.x + NPt.x * rom, Pt.y + NPt.y * rom);
             pmx = fmaxf(pmx, cabs2(Pt));
         }
-        // red[8..15] is not used by the max phase, so no barrier is needed
+        // red[32..47] is not used by the max phase, so no barrier is needed
         // before writing it; nothing read below is rewritten by another
         // thread before the next LED's first barrier (numerators sit in this
         // thread's own half-T slots, tailX was last read in pass A)
         pmx = wave_max(pmx);
-        if (lane == 0) red[8 + w] = pmx;
+        if (lane == 0) red[32 + w] = pmx;
         __syncthreads();
-        float pm2 = red[8];
+        float pm2 = red[32];
 #pragma unroll
-        for (int i = 1; i < NT / 64; ++i) pm2 = fmaxf(pm2, red[8 + i]);
+        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
         pm = sqrtf(pm2);
         FPM_STAMP(6)
     }
@@ -676,14 +784,15 @@ __global__ void __launch_bounds__(fz::NT, 1) k_fused_iteration(FusedArgs a) {
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[i], acc[i]);
 
     // ---- write back the per-patch state
+    loadP();
 #pragma unroll
     for (int j = 0; j < RPG; ++j)
 #pragma unroll
         for (int s = 0; s < 6; ++s)
             if ((inmask[j] >> s) & 1) pup[(kyr[j] + R) * NB + slot_kx(t, s) + R] = P[j][s];
     if (towner) pup[(tp.x + R) * NB + tp.y + R] = Pt;
-    for (int i = tid; i < a.ntiles; i += NT) tmax_g[i] = tmx[i];
-    for (int i = tid; i < a.nwords; i += NT) dirty_g[i] = dirty[i];
+    for (int k = tid; k < a.nbt; k += NT) tmax_g[band_gtile(k)] = tmx[k];
+    for (int i = tid; i < nwords; i += NT) dirty_g[i] = dirty[i];
     if (tid == 0) st.pmax[b] = pm;
 }
 
@@ -725,7 +834,9 @@ struct FusedGeom {
 
 FusedGeom fused_geometry(int np, int r) {
     FusedGeom g;
-    if (np != fz::NP || r < 1 || r > 47) return g;
+    // the tail tables (8 rows, 64 pixels) hold every box row beyond the 64 FFT
+    // rows up to r = 34 (r = 35 has 7 tail rows with more than 64 pixels)
+    if (np != fz::NP || r < 1 || r > 34) return g;
     const int nb = 2 * r + 1;
     const int nfft = nb < fz::NROWS ? nb : fz::NROWS;
     const int extra = nb - nfft;
@@ -746,19 +857,43 @@ FusedGeom fused_geometry(int np, int r) {
     return g;
 }
 
-size_t fused_lds_bytes(int ntiles, int n_tail_rows) {
-    return (size_t)(fz::NG * XTILE + (fz::NROWS + n_tail_rows + 2) * TLD + 256 + 256 + 2 * fz::MAXTAIL) *
-               sizeof(float2) +
-           32 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
-           (size_t)ntiles * sizeof(float) + (size_t)(ntiles + 31) / 32 * sizeof(unsigned);
+size_t fused_lds_bytes(int nt, int nbt, int n_tail_rows) {
+    const int ng = nt / 16, xt = nt > 512 ? 8 * XP : XTILE;
+    return (size_t)(ng * xt + (fz::NROWS + n_tail_rows + 2) * TLD + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
+           48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
+}
+
+struct Band {
+    int bty0, btx0, nbx, nbt;
+};
+Band band_of(const DevState &st) {
+    Band b;
+    b.bty0 = st.sy0 / kTile;
+    b.btx0 = st.sx0 / kTile;
+    b.nbx = st.sx1 / kTile - b.btx0 + 1;
+    b.nbt = b.nbx * (st.sy1 / kTile - b.bty0 + 1);
+    return b;
 }
 }  // namespace
 
-bool fused_supported(int np, int r, int L) {
+// Threads per workgroup of the fused kernel for this geometry: 1024 (4 waves
+// per SIMD) when its LDS fits, else 512, else 0 (fused path unsupported).
+// FPM_FUSED_NT=512 forces the 512-thread variant (A/B measurements).
+int fused_threads(int np, int r, int L, const DevState &st) {
     const FusedGeom g = fused_geometry(np, r);
-    const int ntiles = ((L + kTile - 1) / kTile) * ((L + kTile - 1) / kTile);
-    return g.ok && (L % kTile == 0) && fused_lds_bytes(ntiles, g.n_tail_rows) <= 160 * 1024;
+    if (!g.ok || L % kTile != 0) return 0;
+    if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1) return 0;
+    const Band bd = band_of(st);
+    const char *e = getenv("FPM_FUSED_NT");
+    const bool force512 = e && atoi(e) == 512;
+    if (!force512 && fused_lds_bytes(1024, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 1024;
+    if (fused_lds_bytes(512, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 512;
+    return 0;
 }
+
+// lane-private parking of P and F (1024-thread variant), float2 elements
+size_t fused_park_elems(int nt, int B) { return nt > 512 ? (size_t)B * 2 * 6 * (fz::NROWS / (nt / 16)) * nt : 1; }
 
 size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
@@ -776,9 +911,11 @@ hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, in
 
 hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  unsigned long long *dbg, hipStream_t s) {
+                                  float2 *pscr, int nt, unsigned long long *dbg, hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
-    if (!g.ok) return hipErrorInvalidValue;
+    if (!g.ok || (nt != 512 && nt != 1024)) return hipErrorInvalidValue;
+    if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
+        return hipErrorInvalidValue;
     FusedArgs a;
     a.st = st;
     a.meas_perm = meas_perm;
@@ -786,6 +923,7 @@ hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, co
     a.x0 = x0_dev;
     a.y0 = y0_dev;
     a.tw = tw_np;
+    a.pscr = pscr;
     a.n_order = n_order;
     a.ky_lo = g.ky_lo;
     a.n_fft_rows = g.n_fft_rows;
@@ -804,21 +942,22 @@ hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, co
             }
     }
     for (int i = 0; i < fz::MAXTAIL; ++i) a.tail_px[i] = i < g.n_tail_px ? g.tail_px[i] : make_int2(0, 0);
-    a.ntiles = st.ntx * st.nty;
-    a.nwords = (a.ntiles + 31) / 32;
-    if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
-        return hipErrorInvalidValue;
-    a.bty0 = st.sy0 / kTile;
-    a.btx0 = st.sx0 / kTile;
-    a.nbx = st.sx1 / kTile - a.btx0 + 1;
-    a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
+    const Band bd = band_of(st);
+    a.bty0 = bd.bty0;
+    a.btx0 = bd.btx0;
+    a.nbx = bd.nbx;
+    a.nbt = bd.nbt;
     a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
-    const size_t lds = fused_lds_bytes(a.ntiles, g.n_tail_rows);
-    hipError_t e = hipFuncSetAttribute((const void *)k_fused_iteration, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    const size_t lds = fused_lds_bytes(nt, a.nbt, g.n_tail_rows);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024> : (const void *)k_fused_iteration<512>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_fused_iteration, dim3(st.B), dim3(fz::NT), lds, s, a);
+    if (nt == 1024)
+        hipLaunchKernelGGL(k_fused_iteration<1024>, dim3(st.B), dim3(1024), lds, s, a);
+    else
+        hipLaunchKernelGGL(k_fused_iteration<512>, dim3(st.B), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
