@@ -877,17 +877,20 @@ Band band_of(const DevState &st) {
 }
 }  // namespace
 
-// Threads per workgroup of the fused kernel for this geometry: 1024 (4 waves
-// per SIMD) when its LDS fits, else 512, else 0 (fused path unsupported).
-// FPM_FUSED_NT=512 forces the 512-thread variant (A/B measurements).
+// Threads per workgroup of the fused kernel for this geometry: 512 (2 waves
+// per SIMD), or 0 when its LDS does not fit (fused path unsupported).
+// FPM_FUSED_NT=1024 selects the 4-waves-per-SIMD variant where its LDS fits:
+// measured on MI355X it is SLOWER (14.15 vs 11.67 ms per launch at the metric
+// geometry, profiles/r02_fused_ab.txt): pass B does not speed up with twice
+// the waves (the SIMD's VALU issue, not latency, is what is left), and the
+// half exchange and parked P/F cost extra LDS and scratch traffic.
 int fused_threads(int np, int r, int L, const DevState &st) {
     const FusedGeom g = fused_geometry(np, r);
     if (!g.ok || L % kTile != 0) return 0;
     if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1) return 0;
     const Band bd = band_of(st);
     const char *e = getenv("FPM_FUSED_NT");
-    const bool force512 = e && atoi(e) == 512;
-    if (!force512 && fused_lds_bytes(1024, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 1024;
+    if (e && atoi(e) == 1024 && fused_lds_bytes(1024, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 1024;
     if (fused_lds_bytes(512, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 512;
     return 0;
 }
