@@ -31,6 +31,12 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
                           hipStream_t s);
 // fused path (fpm_fused.hip)
 int fused_threads(int np, int r, int L, const DevState &st);
+// Np 200 fused kernel (fused_mr.hip)
+bool fused_mr_supported(int np, int r, const DevState &st);
+hipError_t fused_mr_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s);
+hipError_t launch_fused_mr_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
+                                     const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
+                                     unsigned long long *dbg, hipStream_t s);
 size_t fused_park_elems(int nt, int B);
 hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s);
 hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
@@ -108,6 +114,7 @@ struct fpm_ctx {
     float *meas_perm = nullptr;     // fused-path layout (reciprocal intensities)
     float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
     int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
+    bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -290,11 +297,13 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
 
     const bool fp16 = (prob->flags & FPM_FLAG_SPEC_FP16) != 0;
     c->fused_nt = fused_threads(np, r, L, st);
-    if (prob->path == FPM_PATH_FUSED && (fp16 || !c->fused_nt))
+    c->fused_mr = !c->fused_nt && fused_mr_supported(np, r, st);
+    const bool fused_ok = c->fused_nt || c->fused_mr;
+    if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_ok))
         return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
                             fp16 ? " with fp16 spectrum storage" : ""));
     c->path = (prob->path == FPM_PATH_GENERAL || fp16) ? FPM_PATH_GENERAL
-              : c->fused_nt                            ? FPM_PATH_FUSED
+              : fused_ok                               ? FPM_PATH_FUSED
                                                        : FPM_PATH_GENERAL;
     // fp16 storage scale: 2^-ceil(log2 Np^2) (fpm_state.hpp)
     int e2 = 0;
@@ -366,7 +375,9 @@ int fpm_set_stream(fpm_ctx *c, void *s) {
 }
 
 static int after_upload(fpm_ctx *c) {
-    if (c->path == FPM_PATH_FUSED)
+    if (c->path == FPM_PATH_FUSED && c->fused_mr)
+        HIP_TRY(fused_mr_permute(c->meas, c->meas_perm, c->prob.n_stack, c->st.B, c->stream));
+    else if (c->path == FPM_PATH_FUSED)
         HIP_TRY(fused_permute(c->meas, c->meas_perm, c->prob.n_stack, c->st.B, c->stream));
     c->uploaded = true;
     c->initialized = false;
@@ -510,7 +521,10 @@ int fpm_run(fpm_ctx *c, int iters) {
     HIP_TRY(hipEventRecord(ev[0], c->stream));
     for (int it = 0; it < iters; ++it) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
-        if (c->path == FPM_PATH_FUSED) {
+        if (c->path == FPM_PATH_FUSED && c->fused_mr) {
+            HIP_TRY(launch_fused_mr_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
+                                              c->prob.n_order, c->tw_np, c->dbg, c->stream));
+        } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->dbg,
                                            c->stream));

@@ -1,0 +1,627 @@
+// fused_mr.hip -- the fused per-patch FPM iteration for Np = 200 (BASELINE
+// config 3, dataset_dogStomach.json literal: Np 200, L 600, naRadius 26):
+// ONE launch per runFPM iteration, one 768-thread workgroup per patch walking
+// every LED of the order (fpmMain.cpp:348-476), the whole per-LED
+// intermediate in LDS.  Same step as fpm_fused.hip (Np 256), with a
+// mixed-radix register transform:
+//
+//   200-point DFT as a 20 x 10 four-step on a 10-lane group: lane l holds
+//   x[l + 10 k], k = 0..19 (the "slot layout").  Stage 1 is a 20-point DFT
+//   over the registers (5 x 4), then the twiddles W200^{l m1}, one LDS
+//   exchange in two rounds (m1 < 10, then m1 >= 10: lane l' reads row l' of a
+//   10 x 10 tile each time), and stage 2 is two 10-point DFTs (5 x 2) per lane
+//   (m1 = l' and m1 = l' + 10).  Their outputs X[m1 + 20 m2] land in register
+//   k = 2 m2 (+1 for m1 = l' + 10): exactly the slot layout again, so the
+//   spatial samples after the inverse and the inputs of the forward transform
+//   share registers, and amplitude replacement needs no data movement.
+//   Six lanes groups per wave (lanes 60..63 idle), 72 groups per workgroup.
+//
+// Support pruning: the pupil box |k| <= r (r <= 29) occupies registers
+// k in {0,1,2,17,18,19} of every lane, so the inverse transforms' inputs and
+// the forward transforms' outputs are pruned to those six "slots".  The
+// whole 200-column T (box rows x 200, 88 KB for r = 26) stays in LDS, so
+// every box row gets its own group (no tail rows) and the row transforms run
+// once per LED.
+//
+// Per LED step, per workgroup:
+//   A  row IDFTs of the box rows of O*P (fpmMain.cpp:358-365) -> T
+//   B  per column x: column IDFT, 1/Np^2, psi' = sqrt(I) psi/|psi + eps|
+//      (eps on Re and Im), column DFT, box rows -> T
+//      (:365-394)
+//   C  row DFTs of the box rows, output-pruned to the support (:394)
+//   update, exact max|objF| from incremental tile maxima, pupil update
+//      (:405-475), as in fpm_fused.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "fft_lds.hpp"
+#include "fpm_state.hpp"
+
+namespace fpm {
+
+namespace fm {
+constexpr int NP = 200;
+constexpr int N1 = 20;   // registers per lane (stage-1 length)
+constexpr int N2 = 10;   // lanes per group (stage-2 length)
+constexpr int GPW = 6;   // groups per wave (lanes 60..63 idle)
+constexpr int NT = 768;  // 12 waves: 3 per SIMD (168-VGPR budget)
+constexpr int NW = NT / 64;
+constexpr int NG = NW * GPW;              // 72 groups >= box rows (r <= 35)
+constexpr int SK[6] = {0, 1, 2, 17, 18, 19};  // registers that can hold |k| <= 29
+constexpr int RMAX = 29;
+constexpr int KYOFF = 32;                 // sig table covers ky in [-32, 31]
+constexpr int XP = 10;                    // exchange-tile row pitch (complex)
+constexpr int XT = 10 * XP;               // exchange tile per group (complex)
+constexpr int TLD = NP + 1;               // T row pitch (complex)
+}  // namespace fm
+
+// ----------------------------------------------------- compile-time twiddles
+constexpr double kPi = 3.14159265358979323846;
+constexpr double ct_sin(double x) {  // |x| <= pi/2 after reduction below
+    double term = x, sum = x;
+    for (int n = 1; n < 14; ++n) {
+        term *= -x * x / ((2.0 * n) * (2.0 * n + 1.0));
+        sum += term;
+    }
+    return sum;
+}
+// exp(-2 pi i j / n) for the forward transform (angle reduced to [0, 2 pi))
+struct CW {
+    float re, im;
+};
+constexpr CW cw(int j, int n) {
+    j %= n;
+    if (j < 0) j += n;
+    double a = 2.0 * kPi * j / n;  // [0, 2 pi)
+    double s = 0, c = 0;
+    if (a <= kPi / 2) {
+        s = ct_sin(a);
+        c = ct_sin(kPi / 2 - a);
+    } else if (a <= kPi) {
+        s = ct_sin(kPi - a);
+        c = -ct_sin(a - kPi / 2);
+    } else if (a <= 3 * kPi / 2) {
+        s = -ct_sin(a - kPi);
+        c = -ct_sin(3 * kPi / 2 - a);
+    } else {
+        s = -ct_sin(2 * kPi - a);
+        c = ct_sin(a - 3 * kPi / 2);
+    }
+    return CW{(float)c, (float)-s};
+}
+// a * W_n^{+-j} with a compile-time twiddle (forward: W = exp(-2 pi i/n))
+template <bool INV, int J, int N>
+__device__ __forceinline__ float2 twc(float2 a) {
+    constexpr CW w = cw(J, N);
+    constexpr float wr = w.re, wi = INV ? -w.im : w.im;
+    if constexpr (J % N == 0) return a;
+    return make_float2(a.x * wr - a.y * wi, a.x * wi + a.y * wr);
+}
+
+// ------------------------------------------------------- register DFTs
+// 10-point DFT, natural order in and out: k = k1 + 2 k2, m = j2 + 5 j1
+template <bool INV>
+__device__ __forceinline__ void dft10(float2 (&v)[10]) {
+    float2 e[5] = {v[0], v[2], v[4], v[6], v[8]}, o[5] = {v[1], v[3], v[5], v[7], v[9]};
+    dft5<INV>(e);
+    dft5<INV>(o);
+    o[1] = twc<INV, 1, 10>(o[1]);
+    o[2] = twc<INV, 2, 10>(o[2]);
+    o[3] = twc<INV, 3, 10>(o[3]);
+    o[4] = twc<INV, 4, 10>(o[4]);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        v[j] = cadd(e[j], o[j]);
+        v[j + 5] = csub(e[j], o[j]);
+    }
+}
+
+// 20-point DFT, natural order in and out: k = k1 + 4 k2 (DFT5 over k2), then
+// W20^{k1 j2}, then DFT4 over k1: m = j2 + 5 j1
+template <bool INV>
+__device__ __forceinline__ void dft20(float2 (&v)[20]) {
+    float2 u[4][5];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+#pragma unroll
+        for (int k2 = 0; k2 < 5; ++k2) u[k1][k2] = v[k1 + 4 * k2];
+        dft5<INV>(u[k1]);
+    }
+    u[1][1] = twc<INV, 1, 20>(u[1][1]);
+    u[1][2] = twc<INV, 2, 20>(u[1][2]);
+    u[1][3] = twc<INV, 3, 20>(u[1][3]);
+    u[1][4] = twc<INV, 4, 20>(u[1][4]);
+    u[2][1] = twc<INV, 2, 20>(u[2][1]);
+    u[2][2] = twc<INV, 4, 20>(u[2][2]);
+    u[2][3] = twc<INV, 6, 20>(u[2][3]);
+    u[2][4] = twc<INV, 8, 20>(u[2][4]);
+    u[3][1] = twc<INV, 3, 20>(u[3][1]);
+    u[3][2] = twc<INV, 6, 20>(u[3][2]);
+    u[3][3] = twc<INV, 9, 20>(u[3][3]);
+    u[3][4] = twc<INV, 12, 20>(u[3][4]);
+#pragma unroll
+    for (int j2 = 0; j2 < 5; ++j2) {
+        float2 b[4] = {u[0][j2], u[1][j2], u[2][j2], u[3][j2]};
+        dft4<INV>(b);
+#pragma unroll
+        for (int j1 = 0; j1 < 4; ++j1) v[j2 + 5 * j1] = b[j1];
+    }
+}
+
+// the same with only v[0,1,2,17,18,19] non-zero (k1,k2) = (0,0),(1,0),(2,0),
+// (1,4),(2,4),(3,4): the DFT5s collapse to one or two terms
+template <bool INV>
+__device__ __forceinline__ void dft20_in6(float2 (&v)[20]) {
+    const float2 a0 = v[0], a1 = v[1], a2 = v[2], b1 = v[17], b2 = v[18], b3 = v[19];
+    float2 u[4][5];
+    // DFT5 of (x, 0, 0, 0, y): U[j] = x + y W5^{4 j}
+#pragma unroll
+    for (int j = 0; j < 5; ++j) u[0][j] = a0;
+    u[1][0] = cadd(a1, b1);
+    u[1][1] = cadd(a1, twc<INV, 4, 5>(b1));
+    u[1][2] = cadd(a1, twc<INV, 8, 5>(b1));
+    u[1][3] = cadd(a1, twc<INV, 12, 5>(b1));
+    u[1][4] = cadd(a1, twc<INV, 16, 5>(b1));
+    u[2][0] = cadd(a2, b2);
+    u[2][1] = cadd(a2, twc<INV, 4, 5>(b2));
+    u[2][2] = cadd(a2, twc<INV, 8, 5>(b2));
+    u[2][3] = cadd(a2, twc<INV, 12, 5>(b2));
+    u[2][4] = cadd(a2, twc<INV, 16, 5>(b2));
+    u[3][0] = b3;
+    u[3][1] = twc<INV, 4, 5>(b3);
+    u[3][2] = twc<INV, 8, 5>(b3);
+    u[3][3] = twc<INV, 12, 5>(b3);
+    u[3][4] = twc<INV, 16, 5>(b3);
+    u[1][1] = twc<INV, 1, 20>(u[1][1]);
+    u[1][2] = twc<INV, 2, 20>(u[1][2]);
+    u[1][3] = twc<INV, 3, 20>(u[1][3]);
+    u[1][4] = twc<INV, 4, 20>(u[1][4]);
+    u[2][1] = twc<INV, 2, 20>(u[2][1]);
+    u[2][2] = twc<INV, 4, 20>(u[2][2]);
+    u[2][3] = twc<INV, 6, 20>(u[2][3]);
+    u[2][4] = twc<INV, 8, 20>(u[2][4]);
+    // u[3][j] = b3 W5^{4j} W20^{3j} = b3 W20^{16j + 3j} = b3 W20^{19 j}
+    u[3][1] = twc<INV, 19, 20>(b3);
+    u[3][2] = twc<INV, 38, 20>(b3);
+    u[3][3] = twc<INV, 57, 20>(b3);
+    u[3][4] = twc<INV, 76, 20>(b3);
+#pragma unroll
+    for (int j2 = 0; j2 < 5; ++j2) {
+        float2 b[4] = {u[0][j2], u[1][j2], u[2][j2], u[3][j2]};
+        dft4<INV>(b);
+#pragma unroll
+        for (int j1 = 0; j1 < 4; ++j1) v[j2 + 5 * j1] = b[j1];
+    }
+}
+
+__device__ __forceinline__ int opaque_i(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// Four-step exchange of a 10-lane group: lane n2 holds U[m1], m1 = 0..19; lane
+// l' receives U_of_lane_j[l'] (za) and U_of_lane_j[l' + 10] (zb), j = 0..9.
+// Two rounds through a 10 x 10 tile (row m1 mod 10 written by all lanes, row
+// l' read by lane l'); LDS operations of one wave execute in issue order and
+// the laundered read base `xrd` keeps the compiler from moving the second
+// round's writes above the first round's reads (see dft16.hpp exchange16).
+__device__ __forceinline__ void xchg10(float2 *tile, int l, int xrd, const float2 (&u)[20], float2 (&za)[10],
+                                       float2 (&zb)[10]) {
+    const float4 *rp = (const float4 *)(tile + xrd);
+#pragma unroll
+    for (int m = 0; m < 10; ++m) tile[m * fm::XP + l] = u[m];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const float4 q = rp[j];
+        za[2 * j] = make_float2(q.x, q.y);
+        za[2 * j + 1] = make_float2(q.z, q.w);
+    }
+#pragma unroll
+    for (int m = 0; m < 10; ++m) tile[m * fm::XP + l] = u[10 + m];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const float4 q = rp[j];
+        zb[2 * j] = make_float2(q.x, q.y);
+        zb[2 * j + 1] = make_float2(q.z, q.w);
+    }
+}
+
+// 200-point DFT in the slot layout (in and out: register k <-> index l + 10 k).
+// INV: inverse (unscaled), only the six SK registers of the input non-zero.
+// Forward: all inputs, only the six SK registers of the output computed.
+// tw2[m1 * 10 + l] = W200^{l m1} (forward), read per use from LDS.
+template <bool INV>
+__device__ __forceinline__ void dft200(float2 (&v)[20], float2 *tile, const float2 *tw2, int l, int xrd) {
+    if (INV) dft20_in6<true>(v);
+    else dft20<false>(v);
+#pragma unroll
+    for (int m1 = 1; m1 < 20; ++m1) {
+        const float2 w = tw2[m1 * 10 + l];
+        v[m1] = cmul(v[m1], INV ? cconj(w) : w);
+    }
+    float2 za[10], zb[10];
+    xchg10(tile, l, xrd, v, za, zb);
+    dft10<INV>(za);
+    dft10<INV>(zb);
+    // X[m1 + 20 m2]: m1 = l' -> register 2 m2, m1 = l' + 10 -> register 2 m2 + 1
+#pragma unroll
+    for (int m2 = 0; m2 < 10; ++m2) {
+        v[2 * m2] = za[m2];
+        v[2 * m2 + 1] = zb[m2];
+    }
+}
+
+struct FusedMRArgs {
+    DevState st;
+    const float *meas_perm;  // [nS][B][x][l][k]: 1/I[l + 10 k][x] (+inf where I = 0)
+    const int *order, *x0, *y0;
+    const float2 *tw;        // exp(-2 pi i k / 200), k < 200
+    int n_order;
+    int btx0, bty0, nbx, nbt;  // live-band tiles (fpm_fused.hip FusedArgs)
+    float rnbx;
+    unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles, else null
+};
+
+__device__ __forceinline__ int mr_slot_k(int s) { return fm::SK[s]; }
+// signed frequency of slot s on lane l: l + 10 SK[s] (- Np for the upper slots)
+__device__ __forceinline__ int mr_kx(int l, int s) { return l + 10 * fm::SK[s] - (fm::SK[s] >= 10 ? fm::NP : 0); }
+
+__global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
+    using namespace fm;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const DevState &st = a.st;
+    const int R = st.r, NB = st.nb, L = st.L;
+    float2 *tiles = sm;                        // NG * XT exchange tiles
+    float2 *th = tiles + NG * XT;              // (NB + 2) * TLD: T rows, zero row, dummy row
+    float2 *tw2 = th + (NB + 2) * TLD;         // [m1][l] = W200^{l m1}
+    float *red = (float *)(tw2 + 200);         // 48
+    int *sig = (int *)(red + 48);              // 64: T row of ky in [-32, 31], -1 outside the box
+    float *tmx = (float *)(sig + 64);          // nbt band-tile maxima
+    unsigned *dirty = (unsigned *)(tmx + a.nbt);
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int gw = lane / N2;                  // group within the wave (6 = idle lanes)
+    const bool act = gw < GPW;
+    const int l = act ? lane - N2 * gw : 0;    // lane within the group
+    const int g = w * GPW + (act ? gw : 0);    // group in the workgroup
+    const int b = blockIdx.x;
+    float2 *tile = tiles + g * XT;
+    const int xrd = opaque_i(l * XP);
+    const int nwords = (a.nbt + 31) >> 5;
+
+    for (int i = tid; i < 200; i += NT) tw2[i] = a.tw[((i / 10) * (i % 10)) % NP];
+    for (int i = tid; i < 64; i += NT) {
+        const int ky = i - KYOFF;
+        sig[i] = (ky >= -R && ky <= R) ? ky + R : -1;
+    }
+    auto band_dy = [&](int k) { return (int)(((float)k + 0.5f) * a.rnbx); };
+    auto band_gtile = [&](int k) {
+        const int dy = band_dy(k);
+        return (a.bty0 + dy) * st.ntx + a.btx0 + (k - dy * a.nbx);
+    };
+    float *tmax_g = st.tmax + (size_t)b * st.ntx * st.nty;
+    unsigned *dirty_g = st.tdirty + (size_t)b * ((st.ntx * st.nty + 31) / 32);
+    for (int k = tid; k < a.nbt; k += NT) tmx[k] = tmax_g[band_gtile(k)];
+    for (int i = tid; i < nwords; i += NT) dirty[i] = dirty_g[i];
+    const int zoff = NB * TLD;
+    for (int i = tid; i < 2 * TLD; i += NT) th[zoff + i] = make_float2(0.f, 0.f);
+
+    float2 *spec = st.spec + (size_t)b * L * L;
+    float2 *pup = st.pupil + (size_t)b * NB * NB;
+    // box row of this group (all box rows are transformed: NG >= NB)
+    const bool ron = act && g < NB;
+    const int kyr = g - R;
+    unsigned inmask = 0;
+    float2 P[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int kx = mr_kx(l, s);
+        const bool in = ron && (kyr * kyr + kx * kx <= R * R);
+        inmask |= (in ? 1u : 0u) << s;
+        P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
+    }
+    __syncthreads();  // sig, tw2
+    // T row offsets of this lane's six column slots (zero row outside the box)
+    int roff[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int kx = mr_kx(l, s);
+        const int sg = (kx >= -KYOFF && kx < KYOFF) ? sig[kx + KYOFF] : -1;
+        roff[s] = sg >= 0 ? sg * TLD : zoff;
+    }
+    float pm = st.pmax[b];
+    const float epsn = st.eps * (float)(NP * NP);
+    const float epsn_im = st.eps_im * (float)(NP * NP);
+
+    unsigned long long acc[kStamps] = {};
+    unsigned long long prev = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+#define FPM_STAMP(i)                                                  \
+    if (a.dbg) {                                                      \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        acc[i] += now_ - prev;                                        \
+        prev = now_;                                                  \
+    }
+    auto window = [&](int itn) {
+        const int ln = a.order[itn];
+        return spec + (unsigned)((a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2);
+    };
+    // slot s of this lane's box row at a compile-time offset from one base
+    auto soff = [](int s) { return 10 * fm::SK[s] - (fm::SK[s] >= 10 ? fm::NP : 0); };
+    auto ldO = [&](const float2 *sr, int s) {
+        const float2 *lr = sr + (kyr * L + l);
+        return ((inmask >> s) & 1) ? lr[soff(s)] : make_float2(0.f, 0.f);
+    };
+    float2 Opre[6];
+    if (a.n_order > 0) {
+        const float2 *sr = window(0);
+#pragma unroll
+        for (int s = 0; s < 6; ++s) Opre[s] = ldO(sr, s);
+    }
+    for (int it = 0; it < a.n_order; ++it) {
+        const int led = a.order[it];
+        const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
+        float2 *srow = spec + (unsigned)(yc * L + xc);
+        const float *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
+        float2 v[20];
+
+        // ---- A: row IDFTs of the box rows of O*P (:358-365) -> T
+        if (ron) {
+#pragma unroll
+            for (int k = 0; k < 20; ++k) v[k] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) v[SK[s]] = cmul(Opre[s], P[s]);
+            dft200<true>(v, tile, tw2, l, xrd);
+            float2 *row = th + g * TLD + l;
+#pragma unroll
+            for (int k = 0; k < 20; ++k) row[10 * k] = v[k];
+        }
+        __syncthreads();  // T complete
+        FPM_STAMP(7)
+
+        // ---- B: columns x = g + NG q: IDFT, amplitude replacement, DFT (:365-394)
+#pragma unroll 1
+        for (int x = g; x < NP; x += NG) {
+            if (!act) break;
+            const uint4 *ip = (const uint4 *)(Ib + (x * N2 + l) * N1);
+            uint4 mi[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) mi[i] = ip[i];
+#pragma unroll
+            for (int k = 0; k < 20; ++k) v[k] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + x];
+            dft200<true>(v, tile, tw2, l, xrd);
+            const unsigned iw[20] = {mi[0].x, mi[0].y, mi[0].z, mi[0].w, mi[1].x, mi[1].y, mi[1].z,
+                                     mi[1].w, mi[2].x, mi[2].y, mi[2].z, mi[2].w, mi[3].x, mi[3].y,
+                                     mi[3].z, mi[3].w, mi[4].x, mi[4].y, mi[4].z, mi[4].w};
+#pragma unroll
+            for (int k = 0; k < 20; ++k) {
+                // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
+                const float invI = __uint_as_float(iw[k]);
+                const float tre = v[k].x + epsn, tim = v[k].y + epsn_im;
+                const float mag2 = __builtin_fmaf(tre, tre, tim * tim);
+                const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
+                v[k] = make_float2(v[k].x * sc, v[k].y * sc);
+            }
+            dft200<false>(v, tile, tw2, l, xrd);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + x] = v[SK[s]];
+        }
+        __syncthreads();
+        FPM_STAMP(2)
+
+        // ---- C: row DFTs of the box rows, output-pruned to the support (:394)
+        float2 F[6];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) Opre[s] = ldO(srow, s);
+        if (ron) {
+            const float2 *row = th + g * TLD + l;
+#pragma unroll
+            for (int k = 0; k < 20; ++k) v[k] = row[10 * k];
+            dft200<false>(v, tile, tw2, l, xrd);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) F[s] = v[SK[s]];
+        } else {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
+        }
+        __syncthreads();  // T rows are reused for the pupil numerator below
+        FPM_STAMP(8)
+
+        // ---- object update on the support (:405-447) and pupil numerator
+        // (:457-464); tile maxima kept exact incrementally (fpm_fused.hip)
+        unsigned *tmu = (unsigned *)tmx;
+        auto note = [&](int py, int px, float ao, float an) {
+            const int ti = ((py >> 4) - a.bty0) * a.nbx + ((px >> 4) - a.btx0);
+            const unsigned cur = tmu[ti];
+            if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
+            if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
+        };
+        if (ron) {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) {
+                const float2 p = P[s], o = Opre[s];
+                const float2 D = csub(F[s], cmul(o, p));  // Objfup - ObjfcropP (:409)
+                const float pa = cmag(p);
+                const float2 kin = upd_coef(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm);
+                const float2 nv = cadd(o, cmul(cmul(D, cscale(cconj(p), pa)), kin));
+                const float oa = cmag(o);
+                const float2 kip = upd_coef(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f);
+                th[g * TLD + s * 10 + l] = cmul(cmul(D, cscale(cconj(o), oa)), kip);
+                if ((inmask >> s) & 1) {
+                    (srow + (kyr * L + l))[soff(s)] = nv;
+                    note(yc + kyr, xc + mr_kx(l, s), oa, cmag(nv));
+                }
+            }
+        }
+        FPM_STAMP(9)
+        __syncthreads();  // spectrum writes, tile maxima, dirty bits
+        if (it + 1 < a.n_order) {
+            const float2 *sr = window(it + 1);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) Opre[s] = ldO(sr, s);
+        }
+        FPM_STAMP(4)
+
+        // ---- exact max|objF| (:460,467) from the band-tile maxima
+        float cm = 0.f, dm = 0.f;
+        for (int k = tid; k < a.nbt; k += NT) {
+            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
+            if (d) dm = fmaxf(dm, tmx[k]);
+            else cm = fmaxf(cm, tmx[k]);
+        }
+        cm = wave_max(cm);
+        dm = wave_max(dm);
+        if (lane == 0) {
+            red[w] = cm;
+            red[16 + w] = dm;
+        }
+        __syncthreads();
+        cm = red[0];
+        dm = red[16];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            cm = fmaxf(cm, red[i]);
+            dm = fmaxf(dm, red[16 + i]);
+        }
+        float omax = cm;
+        if (dm > cm) {  // block-uniform
+            for (int k = w; k < a.nbt; k += NW) {
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;  // wave-uniform
+                const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
+                float mm = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int pp = lane + 64 * jj;
+                    const int yy = ty * 16 + (pp >> 4), xx = tx * 16 + (pp & 15);
+                    if (yy < L && xx < L) mm = fmaxf(mm, cmag(spec[(unsigned)(yy * L + xx)]));
+                }
+                mm = wave_max(mm);
+                if (lane == 0) {
+                    tmx[k] = mm;
+                    atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
+                }
+            }
+            __syncthreads();
+            float m2 = 0.f;
+            for (int k = tid; k < a.nbt; k += NT)
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
+            m2 = wave_max(m2);
+            __syncthreads();
+            if (lane == 0) red[w] = m2;
+            __syncthreads();
+            omax = red[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
+        }
+        FPM_STAMP(5)
+        const float rom = 1.0f / omax;
+        // P += num / max|objF| on the support (:468-475); max|P| for the next LED (:415)
+        float pmx = 0.f;
+        if (ron) {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) {
+                const float2 n = th[g * TLD + s * 10 + l];
+                P[s] = make_float2(P[s].x + n.x * rom, P[s].y + n.y * rom);
+                pmx = fmaxf(pmx, cabs2(P[s]));
+            }
+        }
+        pmx = wave_max(pmx);
+        if (lane == 0) red[32 + w] = pmx;
+        __syncthreads();
+        float pm2 = red[32];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
+        pm = sqrtf(pm2);
+        FPM_STAMP(6)
+    }
+#undef FPM_STAMP
+    if (a.dbg && tid == 0)
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[i], acc[i]);
+
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+        if ((inmask >> s) & 1) pup[(kyr + R) * NB + mr_kx(l, s) + R] = P[s];
+    for (int k = tid; k < a.nbt; k += NT) tmax_g[band_gtile(k)] = tmx[k];
+    for (int i = tid; i < nwords; i += NT) dirty_g[i] = dirty[i];
+    if (tid == 0) st.pmax[b] = pm;
+}
+
+// measurement permutation for Np 200: out[img][x][l][k] = 1 / in[img][l + 10 k][x]
+// (+inf for I = 0), one block per (64-column slab, image), the slab staged in LDS
+__global__ void __launch_bounds__(256) k_permute_meas_mr(const uint16_t *__restrict__ in, float *__restrict__ out,
+                                                         size_t nimg) {
+    __shared__ uint16_t tile[fm::NP][64 + 2];
+    const size_t img = blockIdx.y;
+    if (img >= nimg) return;
+    const int xs = blockIdx.x * 64;
+    const int nx = fm::NP - xs < 64 ? fm::NP - xs : 64;
+    const uint16_t *src = in + img * fm::NP * fm::NP;
+    float *dst = out + img * fm::NP * fm::NP;
+    for (int i = threadIdx.x; i < fm::NP * 64; i += 256) {
+        const int y = i >> 6, x = i & 63;
+        if (x < nx) tile[y][x] = src[(size_t)y * fm::NP + xs + x];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nx * fm::NP; i += 256) {
+        const int x = i / fm::NP, j = i - x * fm::NP;  // j = l * 20 + k
+        const int y = j / fm::N1 + fm::N2 * (j % fm::N1);
+        dst[(size_t)(xs + x) * fm::NP + j] = 1.0f / (float)tile[y][x];
+    }
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+size_t mr_lds_bytes(int nb, int nbt) {
+    return (size_t)(fm::NG * fm::XT + (nb + 2) * fm::TLD + 200) * sizeof(float2) + 48 * sizeof(float) +
+           64 * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
+}
+}  // namespace
+
+// Np 200 fused kernel available for this geometry (r <= 29, T + tiles fit)?
+bool fused_mr_supported(int np, int r, const DevState &st) {
+    if (np != fm::NP || r < 1 || r > fm::RMAX) return false;
+    if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
+        return false;
+    const int bty0 = st.sy0 / kTile, btx0 = st.sx0 / kTile;
+    const int nbx = st.sx1 / kTile - btx0 + 1, nbt = nbx * (st.sy1 / kTile - bty0 + 1);
+    return mr_lds_bytes(2 * r + 1, nbt) <= 160 * 1024;
+}
+
+hipError_t fused_mr_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s) {
+    const size_t nimg = (size_t)n_stack * B;
+    for (size_t i0 = 0; i0 < nimg; i0 += 65535) {
+        const size_t n = (nimg - i0 < 65535) ? nimg - i0 : 65535;
+        hipLaunchKernelGGL(k_permute_meas_mr, dim3((fm::NP + 63) / 64, (unsigned)n), dim3(256), 0, s,
+                           meas + i0 * fm::NP * fm::NP, meas_perm + i0 * fm::NP * fm::NP, n);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_mr_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
+                                     const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
+                                     unsigned long long *dbg, hipStream_t s) {
+    if (!fused_mr_supported(st.np, st.r, st)) return hipErrorInvalidValue;
+    FusedMRArgs a;
+    a.st = st;
+    a.meas_perm = meas_perm;
+    a.order = order_dev;
+    a.x0 = x0_dev;
+    a.y0 = y0_dev;
+    a.tw = tw_np;
+    a.n_order = n_order;
+    a.bty0 = st.sy0 / kTile;
+    a.btx0 = st.sx0 / kTile;
+    a.nbx = st.sx1 / kTile - a.btx0 + 1;
+    a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
+    a.rnbx = 1.0f / (float)a.nbx;
+    a.dbg = dbg;
+    const size_t lds = mr_lds_bytes(st.nb, a.nbt);
+    hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_fused_mr, dim3(st.B), dim3(fm::NT), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fpm
