@@ -341,8 +341,8 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     st.meas = c->meas;
     st.disk = c->disk_dev;
     if (getenv("FPM_STAMPS") && c->path == FPM_PATH_FUSED) {
-        if ((rc = dalloc(c, &c->dbg, kStamps))) return fail(rc);
-        if (hipMemset(c->dbg, 0, kStamps * sizeof(unsigned long long)) != hipSuccess)
+        if ((rc = dalloc(c, &c->dbg, 2 * kStamps))) return fail(rc);
+        if (hipMemset(c->dbg, 0, 2 * kStamps * sizeof(unsigned long long)) != hipSuccess)
             return fail(set_err(FPM_ERR_DEVICE, "memset failed"));
     }
     auto twn = twiddles(np), twl = twiddles(L);
@@ -557,15 +557,17 @@ int fpm_run(fpm_ctx *c, int iters) {
     c->timing.objcrop_ms = crop_ms;
     c->timing.led_launches = (c->path == FPM_PATH_FUSED) ? iters : iters * c->prob.n_order;
     if (c->dbg) {
-        unsigned long long h[kStamps];
+        unsigned long long h[2 * kStamps];
         HIP_TRY(hipMemcpy(h, c->dbg, sizeof h, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemset(c->dbg, 0, sizeof h));
         const double steps = (double)iters * c->prob.n_order * c->st.B;
-        fprintf(stderr, "[fpm stamps] cycles per LED step (wave 0 view, mean over blocks):");
-        const char *names[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre",
-                                      "max",    "P",           "A:rowIDFT", "C:rowDFT",    "upd:body"};
-        for (int i = 0; i < kStamps; ++i) fprintf(stderr, " %s=%.0f", names[i], h[i] / steps);
-        fprintf(stderr, "\n");
+        const char *names[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre", "max",
+                                      "P",      "A:rowIDFT",   "C:rowDFT",  "upd:body",    "B:loop"};
+        for (int v = 0; v < 2; ++v) {
+            fprintf(stderr, "[fpm stamps] cycles per LED step (%s wave view, mean over blocks):", v ? "last" : "first");
+            for (int i = 0; i < kStamps; ++i) fprintf(stderr, " %s=%.0f", names[i], h[v * kStamps + i] / steps);
+            fprintf(stderr, "\n");
+        }
     }
     c->timing.led_launch_ms = c->timing.led_launches ? led_ms / c->timing.led_launches : 0.0;
     return FPM_OK;

@@ -105,6 +105,17 @@ __device__ __forceinline__ int exch_rbase(int t) { return opaque_int(t * XP); }
 // +3%, the strided reads cost more than the halved write count saves)
 __device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
     (void)t;
+#if defined(FPM_EXP_NOXCHG)  // timing experiment only (wrong results): no LDS exchange
+#pragma unroll
+    for (int j = 0; j < 16; ++j) z[j] = y[j ^ 5];
+    return;
+#elif defined(FPM_EXP_WRONLY)  // timing experiment only: writes, no reads
+#pragma unroll
+    for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) z[j] = y[j ^ 5];
+    return;
+#endif
 #pragma unroll
     for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
     if constexpr (XP % 2 == 0) {

@@ -39,6 +39,7 @@
 #include "dft16.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
+#include "fused256.hpp"
 
 namespace fpm {
 
@@ -74,185 +75,6 @@ struct FusedArgs {
     float rnbx;                 // 1 / nbx
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
 };
-
-// 16-point DFT whose input is zero except v[0,1,2,13,14,15]
-template <bool INV>
-__device__ __forceinline__ void dft16_in6(float2 (&v)[16], float2 (&r)[16]) {
-    // stage 1, butterfly k1 over (v[k1], v[k1+4], v[k1+8], v[k1+12])
-    const float2 a0 = v[0], b1 = v[1], b13 = v[13], c2 = v[2], c14 = v[14], d15 = v[15];
-    // k1 = 0: (a0,0,0,0)
-    v[0] = a0; v[4] = a0; v[8] = a0; v[12] = a0;
-    // k1 = 1: (b1,0,0,b13): U[m] = b1 + b13 W4^{3m};  W4^3 = +i forward, -i inverse
-    {
-        const float2 ib = INV ? make_float2(b13.y, -b13.x) : make_float2(-b13.y, b13.x);  // W4^3 * b13
-        v[1] = cadd(b1, b13);
-        v[5] = cadd(b1, ib);
-        v[9] = csub(b1, b13);
-        v[13] = csub(b1, ib);
-    }
-    {
-        const float2 ic = INV ? make_float2(c14.y, -c14.x) : make_float2(-c14.y, c14.x);
-        v[2] = cadd(c2, c14);
-        v[6] = cadd(c2, ic);
-        v[10] = csub(c2, c14);
-        v[14] = csub(c2, ic);
-    }
-    // k1 = 3: (0,0,0,d15): U[m] = d15 W4^{3m}
-    {
-        const float2 id = INV ? make_float2(d15.y, -d15.x) : make_float2(-d15.y, d15.x);
-        v[3] = d15;
-        v[7] = id;
-        v[11] = make_float2(-d15.x, -d15.y);
-        v[15] = make_float2(-id.x, -id.y);
-    }
-    mid_tw<INV>(v);
-#pragma unroll
-    for (int m1 = 0; m1 < 4; ++m1) bf4<INV>(v[4 * m1], v[4 * m1 + 1], v[4 * m1 + 2], v[4 * m1 + 3]);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
-}
-
-// 16-point DFT returning only outputs m in {0,1,2,13,14,15} as o[0..5]
-template <bool INV>
-__device__ __forceinline__ void dft16_out6(float2 (&v)[16], float2 (&o)[6]) {
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) bf4<INV>(v[k1], v[k1 + 4], v[k1 + 8], v[k1 + 12]);
-    mid_tw<INV>(v);
-    // stage 2 over k1 for fixed m1 (positions 4 m1 + k1): y0 = sum, y3 = (a0-a2) - W4(a1-a3)
-    auto y0 = [](float2 a0, float2 a1, float2 a2, float2 a3) { return cadd(cadd(a0, a2), cadd(a1, a3)); };
-    auto y3 = [](float2 a0, float2 a1, float2 a2, float2 a3) {
-        return csub(csub(a0, a2), mul_mi<INV>(csub(a1, a3)));
-    };
-    o[0] = y0(v[0], v[1], v[2], v[3]);                 // m = 0  (m1 0, m2 0)
-    o[1] = y0(v[4], v[5], v[6], v[7]);                 // m = 1  (m1 1, m2 0)
-    o[2] = y0(v[8], v[9], v[10], v[11]);               // m = 2
-    o[3] = y3(v[4], v[5], v[6], v[7]);                 // m = 13 (m1 1, m2 3)
-    o[4] = y3(v[8], v[9], v[10], v[11]);               // m = 14
-    o[5] = y3(v[12], v[13], v[14], v[15]);             // m = 15
-}
-
-// 16-point DFT whose input is zero outside v[8H .. 8H+7] (one half of a row)
-template <bool INV, int H>
-__device__ __forceinline__ void dft16_inhalf(float2 (&v)[16], float2 (&r)[16]) {
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) {
-        if (H == 0) {  // (a0, a1, 0, 0)
-            const float2 a0 = v[k1], a1 = v[k1 + 4], wa1 = mul_mi<INV>(a1);
-            v[k1] = cadd(a0, a1);
-            v[k1 + 4] = cadd(a0, wa1);
-            v[k1 + 8] = csub(a0, a1);
-            v[k1 + 12] = csub(a0, wa1);
-        } else {       // (0, 0, a2, a3)
-            const float2 a2 = v[k1 + 8], a3 = v[k1 + 12], wa3 = mul_mi<INV>(a3);
-            v[k1] = cadd(a2, a3);
-            v[k1 + 4] = make_float2(-a2.x - wa3.x, -a2.y - wa3.y);
-            v[k1 + 8] = csub(a2, a3);
-            v[k1 + 12] = csub(wa3, a2);
-        }
-    }
-    mid_tw<INV>(v);
-#pragma unroll
-    for (int m1 = 0; m1 < 4; ++m1) bf4<INV>(v[4 * m1], v[4 * m1 + 1], v[4 * m1 + 2], v[4 * m1 + 3]);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
-}
-
-// Exchange of the four-step transforms.  NT = 512: the full 16 x 16 tile per
-// group (dft16.hpp exchange16).  NT = 1024: 64 groups' full tiles (147 KB)
-// do not fit beside the half-T, so each group owns HALF a tile (8 rows, 73.7 KB
-// for all groups) and exchanges in two rounds: every lane writes y[0..7],
-// lanes t < 8 read their row; every lane writes y[8..15], lanes t >= 8 read.
-// The second round's writes may not overtake the first round's reads: LDS
-// operations of one wave execute in issue order, and the laundered read base
-// keeps the compiler from reordering them (see exchange16).
-template <bool HALF>
-__device__ __forceinline__ void xchg(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
-    if constexpr (!HALF) {
-        exchange16(scr, t, xrd, y, z);
-    } else {
-        const float4 *rp = (const float4 *)(scr + xrd);  // row (t & 7), 16-B aligned (XP even)
-#pragma unroll
-        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[m1];
-        if (t < 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float4 q = rp[j];
-                z[2 * j] = make_float2(q.x, q.y);
-                z[2 * j + 1] = make_float2(q.z, q.w);
-            }
-        }
-#pragma unroll
-        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[8 + m1];
-        if (t >= 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float4 q = rp[j];
-                z[2 * j] = make_float2(q.x, q.y);
-                z[2 * j + 1] = make_float2(q.z, q.w);
-            }
-        }
-    }
-}
-
-// Four-step twiddles W256^{m t} (m = 0..15) of lane t: held in 32 VGPRs for a
-// whole half (REG, NT = 512: a table read per use serialised on LDS latency at
-// two waves per SIMD) or read from the LDS table tw2[m][t] at each use (NT =
-// 1024: four waves per SIMD hide the latency, and the registers are needed).
-template <bool REG>
-struct Tw;
-template <>
-struct Tw<true> {
-    float2 w[16];
-    __device__ __forceinline__ void load(const float2 *tw2, int t) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m) w[m] = tw2[m * 16 + t];
-    }
-    __device__ __forceinline__ float2 operator[](int m) const { return w[m]; }
-};
-template <>
-struct Tw<false> {
-    const float2 *p;
-    __device__ __forceinline__ void load(const float2 *tw2, int t) { p = tw2 + t; }
-    __device__ __forceinline__ float2 operator[](int m) const { return p[m * 16]; }
-};
-
-// inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six
-// SK registers may be non-zero), output r[m2] = x[t + 16 m2]
-template <bool HALF, class TW>
-__device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const TW &wt, int t,
-                                            int xrd) {
-    float2 y[16];
-    dft16_in6<true>(v, y);
-#pragma unroll
-    for (int m1 = 1; m1 < 16; ++m1) y[m1] = cmul(y[m1], cconj(wt[m1]));
-    xchg<HALF>(scr, t, xrd, y, v);
-    dft16<true>(v, r);
-}
-
-// forward 256-point DFT, input v[n2] = x[t + 16 n2], output o[s] = X[t + 16 SK[s]]
-template <bool HALF, class TW>
-__device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt, int t,
-                                            int xrd) {
-    float2 y[16];
-    dft16<false>(v, y);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
-    xchg<HALF>(scr, t, xrd, y, v);
-    dft16_out6<false>(v, o);
-}
-
-// forward 256-point DFT of a half row (x = t + 16 n2, n2 in [8H, 8H+8), zero
-// elsewhere), output o[s] = X[t + 16 SK[s]]
-template <bool HALF, int H, class TW>
-__device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt, int t,
-                                                   int xrd) {
-    float2 y[16];
-    dft16_inhalf<false, H>(v, y);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], wt[k1]);
-    xchg<HALF>(scr, t, xrd, y, v);
-    dft16_out6<false>(v, o);
-}
 
 // measurement stream: read once per LED, so load it non-temporally and keep
 // L2 for the spectrum window the next LED re-reads
@@ -307,6 +129,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     int *tky = (int *)(tpx + MAXTAIL);              // MAXTAILROWS tail rows
     float *tmx = (float *)(tky + MAXTAILROWS);      // nbt: max|spec| per band tile (upper bound if dirty)
     unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits: tile max may be stale-high
+    int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // pass-B column-block counter
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
@@ -463,14 +286,27 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             // 512 issues the first column before pass A and prefetches one
             // round ahead inside pass B, NT 1024 loads at the top of each round
             constexpr int NQ = TH / (4 * NW);
-            auto colx = [&](int q) { const int r8 = w + NW * q; return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
-            auto ldI = [&](int q, uint4 (&n)[4]) {
-                const uint4 *ip = (const uint4 *)(Ib + ((colx(q) + TH * h) * 16 + t) * 16);
+            // pass B works on 32 column blocks per half: block r8 gives group gg
+            // of a wave column (r8 & 15) + 16 gg + 64 (r8 >> 4)
+            constexpr int NBLK = TH / 4;
+            auto colx = [&](int r8) { return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
+            auto ldI = [&](int xl, uint4 (&n)[4]) {
+                const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * h) * 16 + t) * 16);
+#ifdef FPM_EXP_NOMEAS  // timing experiment only (wrong results): no measurement stream
+                const unsigned u = 0x3f800000u + (unsigned)(xl & 7);
+                for (int i = 0; i < 4; ++i) n[i] = make_uint4(u, u + 1, u + 2, u + 3);
+                (void)ip;
+#else
 #pragma unroll
                 for (int i = 0; i < 4; ++i) n[i] = ld_stream(ip + i);
+#endif
             };
+#ifndef FPM_MEAS_PREF
+#define FPM_MEAS_PREF 0  // 1: one round ahead (measured 5% slower: 16 VGPRs the scheduler needs)
+#endif
+            constexpr bool MPREF = FPM_MEAS_PREF && !PARK;  // measurement prefetched one round ahead
             uint4 nI[4];
-            if (!PARK) ldI(0, nI);
+            if (MPREF) ldI(colx(w), nI);  // this wave's first block is block w
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
             loadP();
             float2 X[RPG][6];
@@ -519,37 +355,55 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 if (p < np_) s2 = cadd(s2, cmul(tailX[p0 + p], wa));
                 th[(NROWS + q) * TLD + xl] = cadd(s2, s3);
             }
+            if (tid == 0) *ccnt = NW;  // pass-B block counter (blocks 0..NW-1 are preassigned)
             __syncthreads();  // half-T complete
             FPM_STAMP(1)
 
             // ---- B: columns x in [128h, 128h+128): IDFT, amplitude replacement, DFT (:365-394)
+            // Column blocks are claimed dynamically (NT 512): wave w starts with
+            // block w and takes the next unclaimed block from an LDS counter.  At
+            // two waves per SIMD the VALU arbiter favours the older wave of each
+            // pair by thousands of cycles over a pass; with a static split the
+            // younger wave then finished its share alone at half the SIMD's issue
+            // rate while the older one waited at the barrier (stamps: 29.8k vs
+            // 44.3k cycles per LED).  The claim for the next block is issued at
+            // the top of a round and consumed after the inverse transform.
             float2 tin[6];
             if (!PARK) {  // the column's six half-T slots, read one round ahead
 #pragma unroll
-                for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(0)];
+                for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(w)];
             }
+            int r8 = w;
 #pragma unroll 1
-            for (int q = 0; q < NQ; ++q) {
-                const int xl = colx(q);
+            for (int q = 0; PARK ? q < NQ : true; ++q) {
+                const int xl = PARK ? colx(w + NW * q) : colx(r8);
                 uint4 cI[4];
+                int nx = 0;
                 if (PARK) {
 #pragma unroll
                     for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xl];
                 } else {
+                    if (lane == 0) nx = atomicAdd(ccnt, 1);
+                    nx = __builtin_amdgcn_readfirstlane(nx);
+                    if (MPREF) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) cI[i] = nI[i];
-                    // unconditional (the last round re-reads its own column) so
-                    // the load is not sunk into a branch at the loop latch
-                    ldI(q + 1 < NQ ? q + 1 : q, nI);
+                        for (int i = 0; i < 4; ++i) cI[i] = nI[i];
+                    } else {
+                        ldI(xl, cI);
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = tin[s];
-                if (PARK) ldI(q, cI);  // FPM_JIT_MEAS experiment: after the inverse transform
+                if (PARK) ldI(xl, cI);
                 idft256_in6<HALF>(v, r, scr, wt, t, xrd);
                 if (!PARK) {
-                    const int xn = colx(q + 1 < NQ ? q + 1 : q);
+                    // next block's measurement and T slots; unconditional (the
+                    // last round re-reads its own column) so the loads are not
+                    // sunk into a branch
+                    const int xn = colx(nx < NBLK ? nx : r8);
+                    if (MPREF) ldI(xn, nI);
 #pragma unroll
                     for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
                 }
@@ -560,16 +414,21 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     const float invI = __uint_as_float(iw[m2]);
                     // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
                     // (cv::add(UMat c2, double) puts eps on both channels, :390)
-                    const float tre = r[m2].x + epsn, tim = r[m2].y + epsn_im;
-                    const float mag2 = __builtin_fmaf(tre, tre, tim * tim);
+                    const pf2 tt = pin(r[m2]) + (pf2){epsn, epsn_im};
+                    const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
                     const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
-                    v[m2] = make_float2(r[m2].x * sc, r[m2].y * sc);
+                    v[m2] = pout(pin(r[m2]) * sc);
                 }
                 float2 o[6];
                 dft256_out6<HALF>(v, o, scr, wt, t, xrd);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
+                if (!PARK) {
+                    if (nx >= NBLK) break;
+                    r8 = nx;
+                }
             }
+            FPM_STAMP(10)  // this wave's own columns done
             __syncthreads();
             FPM_STAMP(2)
 
@@ -780,8 +639,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         FPM_STAMP(6)
     }
 #undef FPM_STAMP
-    if (a.dbg && tid == 0)
-        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[i], acc[i]);
+    // stamps of the first and the last wave (the barrier waits show who is slow)
+    if (a.dbg && (tid == 0 || tid == NT - 64))
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
 
     // ---- write back the per-patch state
     loadP();
@@ -861,7 +721,7 @@ size_t fused_lds_bytes(int nt, int nbt, int n_tail_rows) {
     const int ng = nt / 16, xt = nt > 512 ? 8 * XP : XTILE;
     return (size_t)(ng * xt + (fz::NROWS + n_tail_rows + 2) * TLD + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
-           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + sizeof(int);
 }
 
 struct Band {

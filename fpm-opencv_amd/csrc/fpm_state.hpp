@@ -35,7 +35,7 @@
 namespace fpm {
 
 constexpr int kTile = 16;
-constexpr int kStamps = 10;  // FPM_STAMPS phase counters of the fused kernel
+constexpr int kStamps = 11;  // FPM_STAMPS phase counters of the fused kernel (per recorded wave)
 
 struct DevState {
     float2 *spec;

@@ -408,6 +408,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + x] = v[SK[s]];
         }
+        FPM_STAMP(10)  // this wave's own columns done
         __syncthreads();
         FPM_STAMP(2)
 
@@ -537,8 +538,9 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         FPM_STAMP(6)
     }
 #undef FPM_STAMP
-    if (a.dbg && tid == 0)
-        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[i], acc[i]);
+    // stamps of the first and the last wave (the barrier waits show who is slow)
+    if (a.dbg && (tid == 0 || tid == NT - 64))
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
 
 #pragma unroll
     for (int s = 0; s < 6; ++s)

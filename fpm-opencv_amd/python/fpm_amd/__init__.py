@@ -18,7 +18,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))          # fpm-opencv_amd/
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
-HIP_LIB = os.path.join(LIB_DIR, "libfpm_hip.so")
+# FPM_HIP_LIB: an alternative build of the same library (compiler-flag A/B
+# experiments under tools/gpu/); the default is the in-tree build
+HIP_LIB = os.environ.get("FPM_HIP_LIB") or os.path.join(LIB_DIR, "libfpm_hip.so")
 HOST_LIB = os.path.join(LIB_DIR, "libfpm_host.so")
 
 FPM_OK = 0
