@@ -86,6 +86,27 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
 
 __device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
 
+// Object update and pupil numerator of one support pixel (fpmMain.cpp:405-471),
+// packed FP32: with D = Objfup - ObjfcropP (:409),
+//   O' = O + D conj(P) |P| / ((|P|^2 + d2 + i d2im) max|P|)      (:406-419,433)
+//   num = D conj(O) |O| / (|O|^2 + d1 + i d1im)  (/ max|objF| at the commit)
+// 1/((a + ic) m) = (a - ic) / ((a^2 + c^2) m) and the real factor |P| (|O|)
+// is folded into that coefficient.  |X| is cmag (the tile maxima's function).
+__device__ __forceinline__ float2 slot_update(float2 f, float2 o, float2 p, float pm, const DevState &st,
+                                              float2 &num, float &oa) {
+    const pf2 po = pin(o), pp = pin(p);
+    const pf2 D = pin(f) - pmul(po, pp);
+    const float pa = cmag(p);
+    const float ap = __builtin_fmaf(pa, pa, st.delta2);
+    const float rp = __builtin_amdgcn_rcpf(__builtin_fmaf(ap, ap, st.d2_im * st.d2_im) * pm) * pa;
+    const pf2 nv = po + pmul(pmulc(D, pp), (pf2){ap * rp, -st.d2_im * rp});
+    oa = cmag(o);
+    const float ao = __builtin_fmaf(oa, oa, st.delta1);
+    const float ro = __builtin_amdgcn_rcpf(__builtin_fmaf(ao, ao, st.d1_im * st.d1_im)) * oa;
+    num = pout(pmul(pmulc(D, po), (pf2){ao * ro, -st.d1_im * ro}));
+    return pout(nv);
+}
+
 // half-row intermediate in LDS: row pitch 129 complex, so the 16 lanes of a
 // column read hit 16 different bank pairs
 constexpr int TH = fz::NP / 2;
@@ -271,7 +292,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 
         // ---- gather the sub-aperture on the support (pre-update Objfcrop,
         // fpmMain.cpp:358-362); the tail pixels' O was loaded with Opre
-        if (towner) tailX[tid] = cmul(Ot, Pt);
+        if (towner) tailX[tid] = pout(pmul(pin(Ot), pin(Pt)));
         __syncthreads();  // tailX
         FPM_STAMP(0)
 
@@ -313,7 +334,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) X[j][s] = cmul(Opre[j][s], P[j][s]);   // :364
+                for (int s = 0; s < 6; ++s) X[j][s] = pout(pmul(pin(Opre[j][s]), pin(P[j][s])));   // :364
 #pragma unroll
             for (int j = 0; j < RPG; ++j) {
                 if (!ron[j]) continue;
@@ -332,7 +353,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 }
             }
             FPM_STAMP(7)
-            for (int idx = tid; idx < a.n_tail_rows * TH; idx += NT) {  // tail rows: direct sums
+            // tail rows: direct sums, on the first half of the waves only (the
+            // VALU arbiter favours them, so they finish their rows first)
+            for (int idx = tid; tid < NT / 2 && idx < a.n_tail_rows * TH; idx += NT / 2) {
                 // q is wave-uniform (TH = 2 waves): the row's pixel range comes
                 // from scalar loads; kx runs over a contiguous range, so the
                 // twiddle index advances by x per term
@@ -341,19 +364,20 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 // twiddle W^{-x kx} by recurrence from two table values: a
                 // per-term table read with lane-dependent x conflicts on LDS banks
                 // (even and odd terms on two chains)
+                // (wa, wb hold W^{+x kx}; pmulc applies the conjugate)
                 const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
-                float2 wa = cconj(tw[ti]), wb = cconj(tw[(ti + x) & (NP - 1)]);
-                const float2 wstep = cconj(tw[(2 * x) & (NP - 1)]);
-                float2 s2 = make_float2(0.f, 0.f), s3 = make_float2(0.f, 0.f);
+                pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
+                const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
+                pf2 s2 = {0.f, 0.f}, s3 = {0.f, 0.f};
                 int p = 0;
                 for (; p + 1 < np_; p += 2) {
-                    s2 = cadd(s2, cmul(tailX[p0 + p], wa));
-                    s3 = cadd(s3, cmul(tailX[p0 + p + 1], wb));
-                    wa = cmul(wa, wstep);
-                    wb = cmul(wb, wstep);
+                    s2 += pmulc(pin(tailX[p0 + p]), wa);
+                    s3 += pmulc(pin(tailX[p0 + p + 1]), wb);
+                    wa = pmul(wa, wstep);
+                    wb = pmul(wb, wstep);
                 }
-                if (p < np_) s2 = cadd(s2, cmul(tailX[p0 + p], wa));
-                th[(NROWS + q) * TLD + xl] = cadd(s2, s3);
+                if (p < np_) s2 += pmulc(pin(tailX[p0 + p]), wa);
+                th[(NROWS + q) * TLD + xl] = pout(s2 + s3);
             }
             if (tid == 0) *ccnt = NW;  // pass-B block counter (blocks 0..NW-1 are preassigned)
             __syncthreads();  // half-T complete
@@ -469,19 +493,21 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     for (int s = 0; s < 6; ++s) parkF(j, s) = F[j][s];
             }
             FPM_STAMP(8)
-            for (int pp = g; pp < a.n_tail_px; pp += NG) {  // tail pixels: 16 lanes sum 128 terms
+            // tail pixels: 16 lanes sum 128 terms; first half of the waves only
+            for (int pp = g; g < NG / 2 && pp < a.n_tail_px; pp += NG / 2) {
                 const int2 px = tpx[pp];
                 const float2 *row = th + sig[px.x + KYOFF] * TLD;
                 // W^{x kx} for x = t + 16 m + TH h by recurrence over m (two
                 // table reads instead of eight bank-conflicting ones)
-                float2 s2 = make_float2(0.f, 0.f);
-                float2 wk = tw[((t + TH * h) * (px.y + NP)) & (NP - 1)];
-                const float2 wstep = tw[(16 * (px.y + NP)) & (NP - 1)];
+                pf2 s2p = {0.f, 0.f};
+                pf2 wk = pin(tw[((t + TH * h) * (px.y + NP)) & (NP - 1)]);
+                const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {
-                    s2 = cadd(s2, cmul(row[t + 16 * m], wk));
-                    if (m < 7) wk = cmul(wk, wstep);
+                    s2p += pmul(pin(row[t + 16 * m]), wk);
+                    if (m < 7) wk = pmul(wk, wstep);
                 }
+                float2 s2 = pout(s2p);
 #pragma unroll
                 for (int o = 8; o > 0; o >>= 1) {
                     s2.x += __shfl_xor(s2.x, o, 64);
@@ -517,32 +543,22 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
                 const int kx = slot_kx(t, s);
-                const float2 p = P[j][s], o = Opre[j][s];
-                const float2 D = csub(F[j][s], cmul(o, p));   // Objfup - ObjfcropP (:409)
-                // D |P| P* / ((|P|^2 + d2 + i d2im) max|P|)  (:406-419)
-                const float pa = cmag(p);
-                const float2 kin = upd_coef(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm);
-                const float2 nv = cadd(o, cmul(cmul(D, cscale(cconj(p), pa)), kin));
-                // D |O| O* / (|O|^2 + d1 + i d1im); / max|objF| at the commit (:459-471)
-                const float oa = cmag(o);
-                const float2 kip = upd_coef(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f);
+                float2 num;
+                float oa;
+                const float2 nv = slot_update(F[j][s], Opre[j][s], P[j][s], pm, st, num, oa);
                 // this group's own half-T row is no longer read: park the numerator there
-                th[(g + NG * j) * TLD + s * 16 + t] = cmul(cmul(D, cscale(cconj(o), oa)), kip);
+                th[(g + NG * j) * TLD + s * 16 + t] = num;
                 if ((inmask[j] >> s) & 1) {
                     (srow + (kyr[j] * L + t))[soff(s)] = nv;
                     note(yc + kyr[j], xc + kx, oa, cmag(nv));
                 }
             }
         if (towner) {
-            const float2 p = Pt, o = Ot;
-            const float2 D = csub(tailF[tid], tailX[tid]);
-            const float pa = cmag(p);
-            const float2 kin = upd_coef(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm);
-            const float2 nv = cadd(o, cmul(cmul(D, cscale(cconj(p), pa)), kin));
+            // D = Objfup - ObjfcropP with ObjfcropP = tailX (gathered O*P): pass F = tailF
+            // and the slot helper recomputes O*P the same way the gather did
+            float oa;
+            const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
             srow[tp.x * L + tp.y] = nv;
-            const float oa = cmag(o);
-            const float2 kip = upd_coef(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f);
-            NPt = cmul(cmul(D, cscale(cconj(o), oa)), kip);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
         FPM_STAMP(9)
