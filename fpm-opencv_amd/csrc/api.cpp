@@ -33,16 +33,15 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
 int fused_threads(int np, int r, int L, const DevState &st);
 // Np 200 fused kernel (fused_mr.hip)
 bool fused_mr_supported(int np, int r, const DevState &st);
-hipError_t fused_mr_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s);
-hipError_t launch_fused_mr_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
+hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                      const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                      unsigned long long *dbg, hipStream_t s);
 size_t fused_park_elems(int nt, int B);
-hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s);
-hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
+hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   float2 *pscr, int nt, unsigned long long *dbg, hipStream_t s);
-size_t fused_meas_bytes(int np, int B, int n_stack);
+// in-place measurement layout of the fused kernels (preprocess.hip)
+hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
                                    const int *py0_dev, int bk1x, int bk1y, int bk2x, int bk2y, double bg_threshold,
                                    double dark_mult, bool darkfield, unsigned long long *sums, uint16_t *out,
@@ -111,7 +110,8 @@ struct fpm_ctx {
     float2 *tw_np = nullptr, *tw_L = nullptr;
     float2 *objcrop = nullptr;
     uint16_t *meas = nullptr;
-    float *meas_perm = nullptr;     // fused-path layout (reciprocal intensities)
+    int meas_g = 0;                 // fused paths: meas holds the column layout of meas_layout with
+                                    // g-lane groups (16: Np 256, 10: Np 200) once uploaded; 0: C-ABI
     float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
     int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
@@ -333,8 +333,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
     } else {
-        if ((rc = dalloc(c, &c->meas_perm, fused_meas_bytes(np, B, prob->n_stack) / sizeof(float))))
-            return fail(rc);
+        c->meas_g = c->fused_mr ? 10 : 16;
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
         if ((rc = dalloc(c, &c->pscr, fused_park_elems(c->fused_nt, B)))) return fail(rc);
     }
@@ -375,10 +374,10 @@ int fpm_set_stream(fpm_ctx *c, void *s) {
 }
 
 static int after_upload(fpm_ctx *c) {
-    if (c->path == FPM_PATH_FUSED && c->fused_mr)
-        HIP_TRY(fused_mr_permute(c->meas, c->meas_perm, c->prob.n_stack, c->st.B, c->stream));
-    else if (c->path == FPM_PATH_FUSED)
-        HIP_TRY(fused_permute(c->meas, c->meas_perm, c->prob.n_stack, c->st.B, c->stream));
+    // the fused kernels read the stack column-major, permuted in place (2 B per pixel)
+    if (c->meas_g)
+        HIP_TRY(meas_layout(c->meas, c->st.np, c->meas_g, (size_t)c->prob.n_stack * c->st.B, true, c->stream));
+    c->st.meas_g = c->meas_g;
     c->uploaded = true;
     c->initialized = false;
     return FPM_OK;
@@ -448,7 +447,11 @@ int fpm_download_stack(fpm_ctx *c, uint16_t *meas) {
     if (!c->uploaded) return set_err(FPM_ERR_STATE, "no stack uploaded");
     HIP_TRY(hipSetDevice(c->device));
     const size_t n = (size_t)c->prob.n_stack * c->st.B * c->st.np * c->st.np;
+    const size_t nimg = (size_t)c->prob.n_stack * c->st.B;
+    // back to the C-ABI layout for the copy, then forward again
+    if (c->meas_g) HIP_TRY(meas_layout(c->meas, c->st.np, c->meas_g, nimg, false, c->stream));
     HIP_TRY(hipMemcpyAsync(meas, c->meas, n * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+    if (c->meas_g) HIP_TRY(meas_layout(c->meas, c->st.np, c->meas_g, nimg, true, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return FPM_OK;
 }
@@ -522,10 +525,10 @@ int fpm_run(fpm_ctx *c, int iters) {
     for (int it = 0; it < iters; ++it) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
         if (c->path == FPM_PATH_FUSED && c->fused_mr) {
-            HIP_TRY(launch_fused_mr_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
+            HIP_TRY(launch_fused_mr_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED) {
-            HIP_TRY(launch_fused_iteration(c->st, c->meas_perm, c->order_dev, c->x0_dev, c->y0_dev,
+            HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->dbg,
                                            c->stream));
         } else if (use_graph) {

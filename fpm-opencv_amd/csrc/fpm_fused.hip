@@ -54,7 +54,7 @@ constexpr int KYOFF = 48;                     // sigma table covers ky in [-48, 
 
 struct FusedArgs {
     DevState st;
-    const float *meas_perm;     // [nS][B][x][t][m2]: 1/I[t + 16 m2][x] (+inf where I = 0)
+    const uint16_t *meas;       // [nS][B][x][t][m2] = I[t + 16 m2][x] (meas_layout, preprocess.hip)
     const int *order, *x0, *y0;
     const float2 *tw;           // exp(-2 pi i k / 256), k < 256
     float2 *pscr;               // 1024-thread variant: lane-private parking of P and F
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
         float2 *srow = spec + (unsigned)(yc * L + xc);   // spec[yc + ky][xc + kx] = srow[ky*L + kx]
-        const float *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
+        const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
 
         // ---- gather the sub-aperture on the support (pre-update Objfcrop,
         // fpmMain.cpp:358-362); the tail pixels' O was loaded with Opre
@@ -311,22 +311,17 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             // of a wave column (r8 & 15) + 16 gg + 64 (r8 >> 4)
             constexpr int NBLK = TH / 4;
             auto colx = [&](int r8) { return (r8 & 15) + 16 * gg + 64 * (r8 >> 4); };
-            auto ldI = [&](int xl, uint4 (&n)[4]) {
+            // the lane's 16 uint16 pixels of column x: 32 contiguous bytes
+            auto ldI = [&](int xl, uint4 (&n)[2]) {
                 const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * h) * 16 + t) * 16);
-#ifdef FPM_EXP_NOMEAS  // timing experiment only (wrong results): no measurement stream
-                const unsigned u = 0x3f800000u + (unsigned)(xl & 7);
-                for (int i = 0; i < 4; ++i) n[i] = make_uint4(u, u + 1, u + 2, u + 3);
-                (void)ip;
-#else
 #pragma unroll
-                for (int i = 0; i < 4; ++i) n[i] = ld_stream(ip + i);
-#endif
+                for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
             };
 #ifndef FPM_MEAS_PREF
 #define FPM_MEAS_PREF 0  // 1: one round ahead (measured 5% slower: 16 VGPRs the scheduler needs)
 #endif
             constexpr bool MPREF = FPM_MEAS_PREF && !PARK;  // measurement prefetched one round ahead
-            uint4 nI[4];
+            uint4 nI[2];
             if (MPREF) ldI(colx(w), nI);  // this wave's first block is block w
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
             loadP();
@@ -401,7 +396,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll 1
             for (int q = 0; PARK ? q < NQ : true; ++q) {
                 const int xl = PARK ? colx(w + NW * q) : colx(r8);
-                uint4 cI[4];
+                uint4 cI[2];
                 int nx = 0;
                 if (PARK) {
 #pragma unroll
@@ -411,7 +406,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     nx = __builtin_amdgcn_readfirstlane(nx);
                     if (MPREF) {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) cI[i] = nI[i];
+                        for (int i = 0; i < 2; ++i) cI[i] = nI[i];
                     } else {
                         ldI(xl, cI);
                     }
@@ -431,16 +426,16 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                     for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
                 }
-                const unsigned iw[16] = {cI[0].x, cI[0].y, cI[0].z, cI[0].w, cI[1].x, cI[1].y, cI[1].z, cI[1].w,
-                                         cI[2].x, cI[2].y, cI[2].z, cI[2].w, cI[3].x, cI[3].y, cI[3].z, cI[3].w};
+                const unsigned iw[8] = {cI[0].x, cI[0].y, cI[0].z, cI[0].w, cI[1].x, cI[1].y, cI[1].z, cI[1].w};
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
-                    const float invI = __uint_as_float(iw[m2]);
+                    const float Iv = (float)((m2 & 1) ? (iw[m2 >> 1] >> 16) : (iw[m2 >> 1] & 0xffffu));
                     // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
-                    // (cv::add(UMat c2, double) puts eps on both channels, :390)
+                    // (cv::add(UMat c2, double) puts eps on both channels, :390); I = 0 gives
+                    // 1/I = +inf and a zero scale, the reference's sqrt(0) factor
                     const pf2 tt = pin(r[m2]) + (pf2){epsn, epsn_im};
                     const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
-                    const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
+                    const float sc = __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(Iv));
                     v[m2] = pout(pin(r[m2]) * sc);
                 }
                 float2 o[6];
@@ -672,32 +667,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     if (tid == 0) st.pmax[b] = pm;
 }
 
-// measurement permutation for coalesced column reads, stored as the
-// reciprocal intensity so amplitude replacement is one rsq per pixel:
-// out[s][b][x][t][m2] = 1 / in[s][b][t + 16 m2][x]   (1/0 = +inf: rsq -> 0)
-// One block transposes a 256(y) x 64(x) slab through LDS: coalesced 128-byte
-// row reads, then each output row x (256 contiguous values) is written by
-// consecutive threads.  grid (NP/64, nimg), block 256.
-__global__ void __launch_bounds__(256) k_permute_meas(const uint16_t *__restrict__ in, float *__restrict__ out,
-                                                      size_t nimg) {
-    __shared__ uint16_t tile[fz::NP][64 + 2];
-    const size_t img = blockIdx.y;
-    if (img >= nimg) return;
-    const int xs = blockIdx.x * 64;
-    const uint16_t *src = in + img * fz::NP * fz::NP;
-    float *dst = out + img * fz::NP * fz::NP;
-    for (int i = threadIdx.x; i < fz::NP * 64; i += 256) {
-        const int y = i >> 6, x = i & 63;
-        tile[y][x] = src[(size_t)y * fz::NP + xs + x];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 64 * fz::NP; i += 256) {
-        const int x = i >> 8, j = i & 255;
-        const int y = (j >> 4) + 16 * (j & 15);
-        dst[(size_t)(xs + x) * fz::NP + j] = 1.0f / (float)tile[y][x];
-    }
-}
-
 // ------------------------------------------------------------------ host side
 namespace {
 struct FusedGeom {
@@ -776,19 +745,7 @@ size_t fused_park_elems(int nt, int B) { return nt > 512 ? (size_t)B * 2 * 6 * (
 
 size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
-size_t fused_meas_bytes(int np, int B, int n_stack) { return (size_t)n_stack * B * np * np * sizeof(float); }
-
-hipError_t fused_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s) {
-    const size_t nimg = (size_t)n_stack * B;
-    for (size_t i0 = 0; i0 < nimg; i0 += 65535) {
-        const size_t n = (nimg - i0 < 65535) ? nimg - i0 : 65535;
-        hipLaunchKernelGGL(k_permute_meas, dim3(fz::NP / 64, (unsigned)n), dim3(256), 0, s,
-                           meas + i0 * fz::NP * fz::NP, meas_perm + i0 * fz::NP * fz::NP, n);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
+hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   float2 *pscr, int nt, unsigned long long *dbg, hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
@@ -797,7 +754,7 @@ hipError_t launch_fused_iteration(const DevState &st, const float *meas_perm, co
         return hipErrorInvalidValue;
     FusedArgs a;
     a.st = st;
-    a.meas_perm = meas_perm;
+    a.meas = meas;
     a.order = order_dev;
     a.x0 = x0_dev;
     a.y0 = y0_dev;

@@ -63,6 +63,9 @@ struct DevState {
     // (L/2 +- r) and of the used LEDs ((crop0 + Np/2) +- r), so rows outside
     // [sy0, sy1] and columns outside [sx0, sx1] stay exactly 0 (objCrop skips them)
     int sy0, sy1, sx0, sx1;
+    // layout of meas: 0 = C-ABI [led][patch][y][x]; g > 0 = the fused kernels'
+    // column layout [led][patch][x][t][m] = I[t + g m][x] (meas_layout)
+    int meas_g;
 };
 
 // spectrum element i of patch b (i = y*L + x in the centred spectrum)

@@ -254,7 +254,7 @@ __device__ __forceinline__ void dft200(float2 (&v)[20], float2 *tile, const floa
 
 struct FusedMRArgs {
     DevState st;
-    const float *meas_perm;  // [nS][B][x][l][k]: 1/I[l + 10 k][x] (+inf where I = 0)
+    const uint16_t *meas;    // [nS][B][x][l][k] = I[l + 10 k][x] (meas_layout, preprocess.hip)
     const int *order, *x0, *y0;
     const float2 *tw;        // exp(-2 pi i k / 200), k < 200
     int n_order;
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
         float2 *srow = spec + (unsigned)(yc * L + xc);
-        const float *Ib = a.meas_perm + ((size_t)led * st.B + b) * NP * NP;
+        const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[20];
 
         // ---- A: row IDFTs of the box rows of O*P (:358-365) -> T
@@ -383,8 +383,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll 1
         for (int x = g; x < NP; x += NG) {
             if (!act) break;
-            const uint4 *ip = (const uint4 *)(Ib + (x * N2 + l) * N1);
-            uint4 mi[5];
+            const uint2 *ip = (const uint2 *)(Ib + (x * N2 + l) * N1);  // 20 uint16, 8-B aligned
+            uint2 mi[5];
 #pragma unroll
             for (int i = 0; i < 5; ++i) mi[i] = ip[i];
 #pragma unroll
@@ -392,13 +392,13 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + x];
             dft200<true>(v, tile, tw2, l, xrd);
-            const unsigned iw[20] = {mi[0].x, mi[0].y, mi[0].z, mi[0].w, mi[1].x, mi[1].y, mi[1].z,
-                                     mi[1].w, mi[2].x, mi[2].y, mi[2].z, mi[2].w, mi[3].x, mi[3].y,
-                                     mi[3].z, mi[3].w, mi[4].x, mi[4].y, mi[4].z, mi[4].w};
+            const unsigned iw[10] = {mi[0].x, mi[0].y, mi[1].x, mi[1].y, mi[2].x,
+                                     mi[2].y, mi[3].x, mi[3].y, mi[4].x, mi[4].y};
 #pragma unroll
             for (int k = 0; k < 20; ++k) {
                 // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
-                const float invI = __uint_as_float(iw[k]);
+                const float invI = __builtin_amdgcn_rcpf(
+                    (float)((k & 1) ? (iw[k >> 1] >> 16) : (iw[k >> 1] & 0xffffu)));
                 const float tre = v[k].x + epsn, tim = v[k].y + epsn_im;
                 const float mag2 = __builtin_fmaf(tre, tre, tim * tim);
                 const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
@@ -550,29 +550,6 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     if (tid == 0) st.pmax[b] = pm;
 }
 
-// measurement permutation for Np 200: out[img][x][l][k] = 1 / in[img][l + 10 k][x]
-// (+inf for I = 0), one block per (64-column slab, image), the slab staged in LDS
-__global__ void __launch_bounds__(256) k_permute_meas_mr(const uint16_t *__restrict__ in, float *__restrict__ out,
-                                                         size_t nimg) {
-    __shared__ uint16_t tile[fm::NP][64 + 2];
-    const size_t img = blockIdx.y;
-    if (img >= nimg) return;
-    const int xs = blockIdx.x * 64;
-    const int nx = fm::NP - xs < 64 ? fm::NP - xs : 64;
-    const uint16_t *src = in + img * fm::NP * fm::NP;
-    float *dst = out + img * fm::NP * fm::NP;
-    for (int i = threadIdx.x; i < fm::NP * 64; i += 256) {
-        const int y = i >> 6, x = i & 63;
-        if (x < nx) tile[y][x] = src[(size_t)y * fm::NP + xs + x];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nx * fm::NP; i += 256) {
-        const int x = i / fm::NP, j = i - x * fm::NP;  // j = l * 20 + k
-        const int y = j / fm::N1 + fm::N2 * (j % fm::N1);
-        dst[(size_t)(xs + x) * fm::NP + j] = 1.0f / (float)tile[y][x];
-    }
-}
-
 // ------------------------------------------------------------------ host side
 namespace {
 size_t mr_lds_bytes(int nb, int nbt) {
@@ -591,23 +568,13 @@ bool fused_mr_supported(int np, int r, const DevState &st) {
     return mr_lds_bytes(2 * r + 1, nbt) <= 160 * 1024;
 }
 
-hipError_t fused_mr_permute(const uint16_t *meas, float *meas_perm, int n_stack, int B, hipStream_t s) {
-    const size_t nimg = (size_t)n_stack * B;
-    for (size_t i0 = 0; i0 < nimg; i0 += 65535) {
-        const size_t n = (nimg - i0 < 65535) ? nimg - i0 : 65535;
-        hipLaunchKernelGGL(k_permute_meas_mr, dim3((fm::NP + 63) / 64, (unsigned)n), dim3(256), 0, s,
-                           meas + i0 * fm::NP * fm::NP, meas_perm + i0 * fm::NP * fm::NP, n);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_fused_mr_iteration(const DevState &st, const float *meas_perm, const int *order_dev,
+hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                      const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                      unsigned long long *dbg, hipStream_t s) {
     if (!fused_mr_supported(st.np, st.r, st)) return hipErrorInvalidValue;
     FusedMRArgs a;
     a.st = st;
-    a.meas_perm = meas_perm;
+    a.meas = meas;
     a.order = order_dev;
     a.x0 = x0_dev;
     a.y0 = y0_dev;

@@ -729,12 +729,17 @@ int colw_cw(const FftPlan &pl) {
 }
 
 // sqrt of the init image as complex, fpmMain.cpp:319-322. grid (Np, B)
+// meas in either layout (DevState::meas_g)
 __global__ void k_init_amp(const uint16_t *__restrict__ meas, float2 *__restrict__ out, int np, int B,
-                           int led, size_t out_bs) {
+                           int led, size_t out_bs, int g) {
     const int y = blockIdx.x, b = blockIdx.y;
-    const uint16_t *I = meas + ((size_t)led * B + b) * np * np + (size_t)y * np;
+    const uint16_t *I = meas + ((size_t)led * B + b) * np * np;
     float2 *o = out + (size_t)b * out_bs + (size_t)y * np;
-    for (int x = threadIdx.x; x < np; x += blockDim.x) o[x] = make_float2(sqrtf((float)I[x]), 0.f);
+    const int col = g ? (y % g) * (np / g) + y / g : 0;  // position of row y inside a stored column
+    for (int x = threadIdx.x; x < np; x += blockDim.x) {
+        const uint16_t v = g ? I[(size_t)x * np + col] : I[(size_t)y * np + x];
+        o[x] = make_float2(sqrtf((float)v), 0.f);
+    }
 }
 
 // zero the spectrum, place fftShift(fft2(A) * S) at the centre
@@ -902,7 +907,8 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
                        const float2 *tw_np, hipStream_t s) {
     const int np = st.np;
     const size_t bs = (size_t)np * np;
-    hipLaunchKernelGGL(k_init_amp, dim3(np, st.B), dim3(256), 0, s, st.meas, scratch, np, st.B, init_led, bs);
+    hipLaunchKernelGGL(k_init_amp, dim3(np, st.B), dim3(256), 0, s, st.meas, scratch, np, st.B, init_led, bs,
+                       st.meas_g);
     // fft2: rows then columns, in place (fpmMain.cpp:325)
     hipError_t e = launch_fft_batch(false, scratch, scratch, pl_np, tw_np, np, st.B, bs, np, 1, bs, np, 1, 0, 0,
                                     1.f, s);

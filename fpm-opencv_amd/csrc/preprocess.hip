@@ -79,4 +79,63 @@ hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// In-place measurement layout of the fused paths.  The fused kernels read one
+// image column per 16- (Np 256) or 10-lane (Np 200) group, lane t holding the
+// pixels y = t + G m (m = 0 .. R-1, R = Np / G) -- one contiguous 2R-byte run
+// per lane when the image is stored column-major in that order:
+//     stored[x Np + t R + m] = I[t + G m][x]
+// The stack keeps its uint16 values (2 B per pixel, the C-ABI layout's size):
+// each block stages one whole image in LDS (Np^2 x 2 B <= 128 KiB), then writes
+// it back permuted over itself.  FWD: C-ABI row-major -> fused; !FWD: back.
+namespace {
+template <int NP, int G, bool FWD>
+__global__ void __launch_bounds__(1024) k_meas_layout(uint16_t *meas, size_t nimg) {
+    extern __shared__ uint16_t tl[];  // NP x LD
+    constexpr int R = NP / G, LD = NP + 2;
+    const size_t img = blockIdx.x;
+    if (img >= nimg) return;
+    uint16_t *p = meas + img * NP * NP;
+    for (int i = threadIdx.x; i < NP * NP; i += 1024) {
+        const int a = i / NP, b = i - a * NP;  // FWD: (y, x); !FWD: (x, j)
+        tl[a * LD + b] = p[i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NP * NP; i += 1024) {
+        const int a = i / NP, b = i - a * NP;
+        uint16_t v;
+        if (FWD) {  // destination (x = a, j = b), j = t R + m
+            const int t = b / R, m = b - t * R;
+            v = tl[(t + G * m) * LD + a];
+        } else {    // destination (y = a, x = b)
+            const int t = a % G, m = a / G;
+            v = tl[b * LD + t * R + m];
+        }
+        p[i] = v;
+    }
+}
+
+template <int NP, int G>
+hipError_t launch_layout(uint16_t *meas, size_t nimg, bool fwd, hipStream_t s) {
+    const size_t lds = (size_t)NP * (NP + 2) * sizeof(uint16_t);
+    const void *fn = fwd ? (const void *)k_meas_layout<NP, G, true> : (const void *)k_meas_layout<NP, G, false>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (nimg == 0) return hipSuccess;
+    if (fwd)
+        hipLaunchKernelGGL((k_meas_layout<NP, G, true>), dim3((unsigned)nimg), dim3(1024), lds, s, meas, nimg);
+    else
+        hipLaunchKernelGGL((k_meas_layout<NP, G, false>), dim3((unsigned)nimg), dim3(1024), lds, s, meas, nimg);
+    return hipGetLastError();
+}
+}  // namespace
+
+// g = 16 (Np 256 fused kernel) or 10 (Np 200 fused kernel)
+hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s) {
+    if (np == 256 && g == 16) return launch_layout<256, 16>(meas, nimg, fwd, s);
+    if (np == 200 && g == 10) return launch_layout<200, 10>(meas, nimg, fwd, s);
+    return hipErrorInvalidValue;
+}
+
 }  // namespace fpm
