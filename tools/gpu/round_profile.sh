@@ -21,7 +21,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 python3 tools/prof_summary.py $O/prof $O/kernel_stats.csv
 python3 tools/prof_summary.py $O/prof $O/kernel_stats_fpm.csv "fpm::" > /dev/null
 rm -rf $O/prof   # full traces of the synthetic-input torch kernels exceed gpurun's 64 MiB copy-back
-KRE=${KRE:-"k_fused|k_permute|k_crop"}
+KRE=${KRE:-"k_fused|k_meas_layout|k_crop"}
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \

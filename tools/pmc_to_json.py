@@ -10,8 +10,10 @@ it was measured on; bench.py ignores a file whose hash differs.
 Units and corrections (MI355X_MICROARCH.md, HBM [CDNA4] and PMC notes):
   * FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the
     bytes of 16-B/lane coalesced reads; other widths are uncalibrated.
-    k_permute_meas reads exactly n_img * Np^2 * 2 bytes, so its FETCH ratio
-    calibrates the read side when it is in the same run; otherwise x2.
+    The fused kernels' measurement and spectrum reads are 16-B/lane, so their
+    FETCH is doubled.  k_meas_layout (the one-time in-place layout change)
+    reads exactly n_img * Np^2 * 2 bytes with 2-B/lane reads; its FETCH ratio
+    is reported as a check of the counter, not applied.
   * GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = value / 8.
   * SQ_INSTS_VALU counts wave instructions; a wave64 FP32 VALU instruction
     occupies its SIMD for 2 cycles, so VALU issue fraction =
@@ -35,7 +37,7 @@ N_SIMD = 1024
 
 
 def short(name):
-    for k in ("k_fused_iteration", "k_permute_meas", "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows",
+    for k in ("k_fused_iteration", "k_fused_mr", "k_meas_layout", "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows",
               "k_crop_cols", "k_colpass_wave", "k_colpass_tiled", "k_gather_rowifft_tiled",
               "k_rowfft_update_tiled", "k_tile_rows", "k_pupil_commit"):
         if k in name:
@@ -71,28 +73,27 @@ def derive(c):
 def main():
     src, out = sys.argv[1], sys.argv[2]
     acc = defaultdict(lambda: defaultdict(list))
-    perm = []  # (work-items, FETCH bytes) per k_permute_meas dispatch
+    perm = []  # (work-items, FETCH bytes) per k_meas_layout dispatch
     for f in sorted(glob.glob(os.path.join(src, "*", "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 k = short(r["Kernel_Name"])
                 v = float(r["Counter_Value"])
                 acc[k][r["Counter_Name"]].append(v)
-                if k == "k_permute_meas" and r["Counter_Name"] == "FETCH_SIZE":
+                if k == "k_meas_layout" and r["Counter_Name"] == "FETCH_SIZE":
                     perm.append((int(r["Grid_Size"]), v * 1024.0))
     raw = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
     res = {"src_hash": src_hash(), "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
            "derived": {}}
-    cal = None
     if perm:
-        # grid (Np/64, n_img) x 256 threads at Np 256: work-items = 4 * 256 * n_img
+        # grid n_img x 1024 threads, one Np 256 image (128 KiB) per block
         np_ = 256
-        known = sum(g // (np_ // 64 * 256) * np_ * np_ * 2.0 for g, _ in perm)
-        cal = known / sum(v for _, v in perm)
-        res["permute_known_read_bytes"] = known
+        known = sum(g // 1024 * np_ * np_ * 2.0 for g, _ in perm)
+        res["layout_known_read_bytes"] = known
+        res["layout_fetch_ratio"] = known / sum(v for _, v in perm)
     for k, d in raw.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            scale = cal if (k == "k_fused_iteration" and cal) else 2.0
+            scale = 2.0
             res["read_scale"][k] = scale
             res["per_launch_hbm_bytes"][k] = d["FETCH_SIZE"] * 1024.0 * scale + d["WRITE_SIZE"] * 1024.0
         dv = derive(d)
