@@ -35,8 +35,11 @@
 
 #include <cstdlib>
 
+#include "cpk.hpp"
+#include "dft200.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
+#include "update.hpp"
 
 namespace fpm {
 
@@ -55,202 +58,6 @@ constexpr int XP = 10;                    // exchange-tile row pitch (complex)
 constexpr int XT = 10 * XP;               // exchange tile per group (complex)
 constexpr int TLD = NP + 1;               // T row pitch (complex)
 }  // namespace fm
-
-// ----------------------------------------------------- compile-time twiddles
-constexpr double kPi = 3.14159265358979323846;
-constexpr double ct_sin(double x) {  // |x| <= pi/2 after reduction below
-    double term = x, sum = x;
-    for (int n = 1; n < 14; ++n) {
-        term *= -x * x / ((2.0 * n) * (2.0 * n + 1.0));
-        sum += term;
-    }
-    return sum;
-}
-// exp(-2 pi i j / n) for the forward transform (angle reduced to [0, 2 pi))
-struct CW {
-    float re, im;
-};
-constexpr CW cw(int j, int n) {
-    j %= n;
-    if (j < 0) j += n;
-    double a = 2.0 * kPi * j / n;  // [0, 2 pi)
-    double s = 0, c = 0;
-    if (a <= kPi / 2) {
-        s = ct_sin(a);
-        c = ct_sin(kPi / 2 - a);
-    } else if (a <= kPi) {
-        s = ct_sin(kPi - a);
-        c = -ct_sin(a - kPi / 2);
-    } else if (a <= 3 * kPi / 2) {
-        s = -ct_sin(a - kPi);
-        c = -ct_sin(3 * kPi / 2 - a);
-    } else {
-        s = -ct_sin(2 * kPi - a);
-        c = ct_sin(a - 3 * kPi / 2);
-    }
-    return CW{(float)c, (float)-s};
-}
-// a * W_n^{+-j} with a compile-time twiddle (forward: W = exp(-2 pi i/n))
-template <bool INV, int J, int N>
-__device__ __forceinline__ float2 twc(float2 a) {
-    constexpr CW w = cw(J, N);
-    constexpr float wr = w.re, wi = INV ? -w.im : w.im;
-    if constexpr (J % N == 0) return a;
-    return make_float2(a.x * wr - a.y * wi, a.x * wi + a.y * wr);
-}
-
-// ------------------------------------------------------- register DFTs
-// 10-point DFT, natural order in and out: k = k1 + 2 k2, m = j2 + 5 j1
-template <bool INV>
-__device__ __forceinline__ void dft10(float2 (&v)[10]) {
-    float2 e[5] = {v[0], v[2], v[4], v[6], v[8]}, o[5] = {v[1], v[3], v[5], v[7], v[9]};
-    dft5<INV>(e);
-    dft5<INV>(o);
-    o[1] = twc<INV, 1, 10>(o[1]);
-    o[2] = twc<INV, 2, 10>(o[2]);
-    o[3] = twc<INV, 3, 10>(o[3]);
-    o[4] = twc<INV, 4, 10>(o[4]);
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        v[j] = cadd(e[j], o[j]);
-        v[j + 5] = csub(e[j], o[j]);
-    }
-}
-
-// 20-point DFT, natural order in and out: k = k1 + 4 k2 (DFT5 over k2), then
-// W20^{k1 j2}, then DFT4 over k1: m = j2 + 5 j1
-template <bool INV>
-__device__ __forceinline__ void dft20(float2 (&v)[20]) {
-    float2 u[4][5];
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) {
-#pragma unroll
-        for (int k2 = 0; k2 < 5; ++k2) u[k1][k2] = v[k1 + 4 * k2];
-        dft5<INV>(u[k1]);
-    }
-    u[1][1] = twc<INV, 1, 20>(u[1][1]);
-    u[1][2] = twc<INV, 2, 20>(u[1][2]);
-    u[1][3] = twc<INV, 3, 20>(u[1][3]);
-    u[1][4] = twc<INV, 4, 20>(u[1][4]);
-    u[2][1] = twc<INV, 2, 20>(u[2][1]);
-    u[2][2] = twc<INV, 4, 20>(u[2][2]);
-    u[2][3] = twc<INV, 6, 20>(u[2][3]);
-    u[2][4] = twc<INV, 8, 20>(u[2][4]);
-    u[3][1] = twc<INV, 3, 20>(u[3][1]);
-    u[3][2] = twc<INV, 6, 20>(u[3][2]);
-    u[3][3] = twc<INV, 9, 20>(u[3][3]);
-    u[3][4] = twc<INV, 12, 20>(u[3][4]);
-#pragma unroll
-    for (int j2 = 0; j2 < 5; ++j2) {
-        float2 b[4] = {u[0][j2], u[1][j2], u[2][j2], u[3][j2]};
-        dft4<INV>(b);
-#pragma unroll
-        for (int j1 = 0; j1 < 4; ++j1) v[j2 + 5 * j1] = b[j1];
-    }
-}
-
-// the same with only v[0,1,2,17,18,19] non-zero (k1,k2) = (0,0),(1,0),(2,0),
-// (1,4),(2,4),(3,4): the DFT5s collapse to one or two terms
-template <bool INV>
-__device__ __forceinline__ void dft20_in6(float2 (&v)[20]) {
-    const float2 a0 = v[0], a1 = v[1], a2 = v[2], b1 = v[17], b2 = v[18], b3 = v[19];
-    float2 u[4][5];
-    // DFT5 of (x, 0, 0, 0, y): U[j] = x + y W5^{4 j}
-#pragma unroll
-    for (int j = 0; j < 5; ++j) u[0][j] = a0;
-    u[1][0] = cadd(a1, b1);
-    u[1][1] = cadd(a1, twc<INV, 4, 5>(b1));
-    u[1][2] = cadd(a1, twc<INV, 8, 5>(b1));
-    u[1][3] = cadd(a1, twc<INV, 12, 5>(b1));
-    u[1][4] = cadd(a1, twc<INV, 16, 5>(b1));
-    u[2][0] = cadd(a2, b2);
-    u[2][1] = cadd(a2, twc<INV, 4, 5>(b2));
-    u[2][2] = cadd(a2, twc<INV, 8, 5>(b2));
-    u[2][3] = cadd(a2, twc<INV, 12, 5>(b2));
-    u[2][4] = cadd(a2, twc<INV, 16, 5>(b2));
-    u[3][0] = b3;
-    u[3][1] = twc<INV, 4, 5>(b3);
-    u[3][2] = twc<INV, 8, 5>(b3);
-    u[3][3] = twc<INV, 12, 5>(b3);
-    u[3][4] = twc<INV, 16, 5>(b3);
-    u[1][1] = twc<INV, 1, 20>(u[1][1]);
-    u[1][2] = twc<INV, 2, 20>(u[1][2]);
-    u[1][3] = twc<INV, 3, 20>(u[1][3]);
-    u[1][4] = twc<INV, 4, 20>(u[1][4]);
-    u[2][1] = twc<INV, 2, 20>(u[2][1]);
-    u[2][2] = twc<INV, 4, 20>(u[2][2]);
-    u[2][3] = twc<INV, 6, 20>(u[2][3]);
-    u[2][4] = twc<INV, 8, 20>(u[2][4]);
-    // u[3][j] = b3 W5^{4j} W20^{3j} = b3 W20^{16j + 3j} = b3 W20^{19 j}
-    u[3][1] = twc<INV, 19, 20>(b3);
-    u[3][2] = twc<INV, 38, 20>(b3);
-    u[3][3] = twc<INV, 57, 20>(b3);
-    u[3][4] = twc<INV, 76, 20>(b3);
-#pragma unroll
-    for (int j2 = 0; j2 < 5; ++j2) {
-        float2 b[4] = {u[0][j2], u[1][j2], u[2][j2], u[3][j2]};
-        dft4<INV>(b);
-#pragma unroll
-        for (int j1 = 0; j1 < 4; ++j1) v[j2 + 5 * j1] = b[j1];
-    }
-}
-
-__device__ __forceinline__ int opaque_i(int v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-
-// Four-step exchange of a 10-lane group: lane n2 holds U[m1], m1 = 0..19; lane
-// l' receives U_of_lane_j[l'] (za) and U_of_lane_j[l' + 10] (zb), j = 0..9.
-// Two rounds through a 10 x 10 tile (row m1 mod 10 written by all lanes, row
-// l' read by lane l'); LDS operations of one wave execute in issue order and
-// the laundered read base `xrd` keeps the compiler from moving the second
-// round's writes above the first round's reads (see dft16.hpp exchange16).
-__device__ __forceinline__ void xchg10(float2 *tile, int l, int xrd, const float2 (&u)[20], float2 (&za)[10],
-                                       float2 (&zb)[10]) {
-    const float4 *rp = (const float4 *)(tile + xrd);
-#pragma unroll
-    for (int m = 0; m < 10; ++m) tile[m * fm::XP + l] = u[m];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const float4 q = rp[j];
-        za[2 * j] = make_float2(q.x, q.y);
-        za[2 * j + 1] = make_float2(q.z, q.w);
-    }
-#pragma unroll
-    for (int m = 0; m < 10; ++m) tile[m * fm::XP + l] = u[10 + m];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const float4 q = rp[j];
-        zb[2 * j] = make_float2(q.x, q.y);
-        zb[2 * j + 1] = make_float2(q.z, q.w);
-    }
-}
-
-// 200-point DFT in the slot layout (in and out: register k <-> index l + 10 k).
-// INV: inverse (unscaled), only the six SK registers of the input non-zero.
-// Forward: all inputs, only the six SK registers of the output computed.
-// tw2[m1 * 10 + l] = W200^{l m1} (forward), read per use from LDS.
-template <bool INV>
-__device__ __forceinline__ void dft200(float2 (&v)[20], float2 *tile, const float2 *tw2, int l, int xrd) {
-    if (INV) dft20_in6<true>(v);
-    else dft20<false>(v);
-#pragma unroll
-    for (int m1 = 1; m1 < 20; ++m1) {
-        const float2 w = tw2[m1 * 10 + l];
-        v[m1] = cmul(v[m1], INV ? cconj(w) : w);
-    }
-    float2 za[10], zb[10];
-    xchg10(tile, l, xrd, v, za, zb);
-    dft10<INV>(za);
-    dft10<INV>(zb);
-    // X[m1 + 20 m2]: m1 = l' -> register 2 m2, m1 = l' + 10 -> register 2 m2 + 1
-#pragma unroll
-    for (int m2 = 0; m2 < 10; ++m2) {
-        v[2 * m2] = za[m2];
-        v[2 * m2 + 1] = zb[m2];
-    }
-}
 
 struct FusedMRArgs {
     DevState st;
@@ -279,6 +86,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     int *sig = (int *)(red + 48);              // 64: T row of ky in [-32, 31], -1 outside the box
     float *tmx = (float *)(sig + 64);          // nbt band-tile maxima
     unsigned *dirty = (unsigned *)(tmx + a.nbt);
+    int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // pass-B column-block counter
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int gw = lane / N2;                  // group within the wave (6 = idle lanes)
@@ -370,19 +178,29 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
             for (int k = 0; k < 20; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int s = 0; s < 6; ++s) v[SK[s]] = cmul(Opre[s], P[s]);
-            dft200<true>(v, tile, tw2, l, xrd);
+            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));
+            dft200<true, true>(v, tile, tw2, l, xrd);
             float2 *row = th + g * TLD + l;
 #pragma unroll
             for (int k = 0; k < 20; ++k) row[10 * k] = v[k];
         }
+        if (tid == 0) *ccnt = NW;  // pass-B block counter (blocks 0..NW-1 are preassigned)
         __syncthreads();  // T complete
         FPM_STAMP(7)
 
-        // ---- B: columns x = g + NG q: IDFT, amplitude replacement, DFT (:365-394)
+        // ---- B: IDFT, amplitude replacement, DFT per column (:365-394).  Column
+        // blocks of GPW: block c gives group gw of a wave column GPW c + gw; wave w
+        // starts with block w and claims the next from an LDS counter (the VALU
+        // arbiter's age order makes a static split finish unevenly, fpm_fused.hip)
+        constexpr int NBLK = (NP + GPW - 1) / GPW;
+        int cb = w;
 #pragma unroll 1
-        for (int x = g; x < NP; x += NG) {
-            if (!act) break;
+        while (true) {
+            int nx = 0;
+            if (lane == 0) nx = atomicAdd(ccnt, 1);
+            nx = __builtin_amdgcn_readfirstlane(nx);
+            const int x = GPW * cb + gw;
+            if (act && x < NP) {
             const uint2 *ip = (const uint2 *)(Ib + (x * N2 + l) * N1);  // 20 uint16, 8-B aligned
             uint2 mi[5];
 #pragma unroll
@@ -391,7 +209,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             for (int k = 0; k < 20; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
             for (int s = 0; s < 6; ++s) v[SK[s]] = th[roff[s] + x];
-            dft200<true>(v, tile, tw2, l, xrd);
+            dft200<true, true>(v, tile, tw2, l, xrd);
             const unsigned iw[10] = {mi[0].x, mi[0].y, mi[1].x, mi[1].y, mi[2].x,
                                      mi[2].y, mi[3].x, mi[3].y, mi[4].x, mi[4].y};
 #pragma unroll
@@ -399,14 +217,17 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
                 // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
                 const float invI = __builtin_amdgcn_rcpf(
                     (float)((k & 1) ? (iw[k >> 1] >> 16) : (iw[k >> 1] & 0xffffu)));
-                const float tre = v[k].x + epsn, tim = v[k].y + epsn_im;
-                const float mag2 = __builtin_fmaf(tre, tre, tim * tim);
+                const pf2 tt = pin(v[k]) + (pf2){epsn, epsn_im};
+                const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
                 const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
-                v[k] = make_float2(v[k].x * sc, v[k].y * sc);
+                v[k] = pout(pin(v[k]) * sc);
             }
-            dft200<false>(v, tile, tw2, l, xrd);
+            dft200<false, false>(v, tile, tw2, l, xrd);
 #pragma unroll
             for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + x] = v[SK[s]];
+            }
+            if (nx >= NBLK) break;
+            cb = nx;
         }
         FPM_STAMP(10)  // this wave's own columns done
         __syncthreads();
@@ -420,7 +241,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             const float2 *row = th + g * TLD + l;
 #pragma unroll
             for (int k = 0; k < 20; ++k) v[k] = row[10 * k];
-            dft200<false>(v, tile, tw2, l, xrd);
+            dft200<false, false>(v, tile, tw2, l, xrd);
 #pragma unroll
             for (int s = 0; s < 6; ++s) F[s] = v[SK[s]];
         } else {
@@ -442,14 +263,10 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         if (ron) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                const float2 p = P[s], o = Opre[s];
-                const float2 D = csub(F[s], cmul(o, p));  // Objfup - ObjfcropP (:409)
-                const float pa = cmag(p);
-                const float2 kin = upd_coef(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm);
-                const float2 nv = cadd(o, cmul(cmul(D, cscale(cconj(p), pa)), kin));
-                const float oa = cmag(o);
-                const float2 kip = upd_coef(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f);
-                th[g * TLD + s * 10 + l] = cmul(cmul(D, cscale(cconj(o), oa)), kip);
+                float2 num;
+                float oa;
+                const float2 nv = slot_update(F[s], Opre[s], P[s], pm, st, num, oa);
+                th[g * TLD + s * 10 + l] = num;
                 if ((inmask >> s) & 1) {
                     (srow + (kyr * L + l))[soff(s)] = nv;
                     note(yc + kyr, xc + mr_kx(l, s), oa, cmag(nv));
@@ -554,7 +371,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 namespace {
 size_t mr_lds_bytes(int nb, int nbt) {
     return (size_t)(fm::NG * fm::XT + (nb + 2) * fm::TLD + 200) * sizeof(float2) + 48 * sizeof(float) +
-           64 * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
+           64 * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) +
+           sizeof(int);
 }
 }  // namespace
 

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dft16.hpp"
+#include "dft200.hpp"
 #include "fpm_state.hpp"
 
 #ifndef FPM_CROP_UNROLL
@@ -225,6 +226,167 @@ hipError_t launch_crop(const DevState &st, float2 *out, const float2 *tw_L, hipS
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ L = 600 (= 200 x 3)
+// BASELINE config 3 (Np 200, resImprovementFactor 3).  One 600-point transform
+// per 10-lane group (dft200.hpp, six groups per wave, lanes 60..63 idle):
+//   x[i], i = 3 m + c (c < 3, m < 200): Y_c = DFT200(x[3 m + c]), lane l
+//   holding m = l + 10 k (k < 20); then the lane-local radix-3 combine
+//   X[k' + 200 p] = sum_c W600^{c k'} W3^{c p} Y_c[k'],  k' = l + 10 k.
+// fftShift: the element roll by L/2 = 300 = 3 * 100 is the register relabel
+// k -> k + 10 (mod 20); the row roll is the source row, as for L = 256 M.
+namespace c600 {
+constexpr int L = 600, H = 300, GPW = 6;
+
+// x[c][k] = element 3 (l + 10 k) + c; on return x[p][k] = X[l + 10 k + 200 p]
+template <bool INV>
+__device__ __forceinline__ void dft600_regs(float2 (&x)[3][20], float2 *tile, const float2 *tw2, const float2 *twL,
+                                            int l, int xrd) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dft200<INV, false>(x[c], tile, tw2, l, xrd);
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+        const int kp = l + 10 * k;
+        float2 z[3];
+        z[0] = x[0][k];
+        const float2 w1 = twL[kp], w2 = twL[2 * kp];
+        z[1] = pout(INV ? pmulc(pin(x[1][k]), pin(w1)) : pmul(pin(x[1][k]), pin(w1)));
+        z[2] = pout(INV ? pmulc(pin(x[2][k]), pin(w2)) : pmul(pin(x[2][k]), pin(w2)));
+        dft3<INV>(z);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) x[p][k] = z[p];
+    }
+}
+
+// W600 table and the four-step table tw2[m1][l] = W200^{l m1} = W600^{3 l m1}
+__device__ __forceinline__ void load_tw600(float2 *twL, float2 *tw2, const float2 *__restrict__ tw_L) {
+    for (int i = threadIdx.x; i < L; i += blockDim.x) twL[i] = tw_L[i];
+    for (int i = threadIdx.x; i < 200; i += blockDim.x) tw2[i] = tw_L[(3 * (i / 10) * (i % 10)) % L];
+    __syncthreads();
+}
+
+// pass 1: row IDFTs of the live spectrum rows (see k_crop_rows).  grid
+// (ceil(nlive / (6 W)), B), block 64 W
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_crop_rows600(const float2 *__restrict__ spec, float2 *__restrict__ out,
+                                                         const float2 *__restrict__ tw_L, int sy0, int sy1, int sx0,
+                                                         int sx1) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2 *twL = sm, *tw2 = sm + L, *tiles = tw2 + 200;  // 6 W exchange tiles of 100 + a dummy
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gw = lane / 10;
+    const bool act = gw < GPW;
+    const int l = act ? lane - 10 * gw : 0, g = w * GPW + (act ? gw : 0);
+    // lanes 60..63 run the transform too (no divergence); their exchange goes
+    // to a dummy tile so it cannot race with group 0's
+    float2 *tile = tiles + (act ? g : GPW * W) * 100;
+    const int xrd = opaque_i(l * kXP10);
+    load_tw600(twL, tw2, tw_L);
+    const int b = blockIdx.y, srow = sy0 + blockIdx.x * GPW * W + g;
+    const bool live = act && srow <= sy1;
+    const int row = srow + H < L ? srow + H : srow - H;  // objF row = spec row + L/2
+    const float2 *src = spec + (size_t)b * L * L + (size_t)(srow <= sy1 ? srow : sy1) * L;
+    float2 x[3][20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {  // element roll by L/2: register k -> k + 10
+            const int sc = 3 * (l + 10 * k) + c;
+            x[c][(k + 10) % 20] = in_band(sc, sx0, sx1) ? src[sc] : make_float2(0.f, 0.f);
+        }
+    dft600_regs<true>(x, tile, tw2, twL, l, xrd);
+    if (!live) return;
+    float2 *dst = out + (size_t)b * L * L + (size_t)row * L;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int k = 0; k < 20; ++k) dst[l + 10 * k + 200 * p] = x[p][k];
+}
+
+// pass 2: column IDFTs in place, scaled 1/L^2, one strip of G = 6 W columns
+// per block staged through LDS in two halves of 300 rows (see k_crop_cols).
+// Half h holds input registers k in [10 h, 10 h + 10) (element 3 (l + 10 k) + c
+// >= 300 iff k >= 10) and output registers with 10 k + 200 p >= 300.
+// grid (ceil(L / G), B), block 64 W
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
+                                                         float scale, int sy0, int sy1) {
+    constexpr int G = GPW * W, SP = G + 1;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2 *twL = sm, *tw2 = sm + L, *strip = tw2 + 200;  // H x SP
+    float2 *tiles = strip;  // exchange tiles inside the strip: used only while every column is in registers
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gw = lane / 10;
+    const bool act = gw < GPW;
+    const int l = act ? lane - 10 * gw : 0, g = w * GPW + (act ? gw : 0);
+    float2 *tile = tiles + (act ? g : G) * 100;  // lanes 60..63: dummy tile (see k_crop_rows600)
+    const int xrd = opaque_i(l * kXP10);
+    load_tw600(twL, tw2, tw_L);
+    const int b = blockIdx.y, c0 = blockIdx.x * G;
+    const int ncol = L - c0 < G ? L - c0 : G;
+    const bool colok = act && g < ncol;
+    float2 *base = io + (size_t)b * L * L + c0;
+    constexpr int NTH = 64 * W;
+    float2 x[3][20];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        // objF row y + h H is spec row y + (1 - h) H: live rows of this half
+        const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
+        for (int idx = ya * G + threadIdx.x; idx < (yb + 1) * G; idx += NTH) {
+            const int y = idx / G, cc = idx - y * G;
+            if (cc < ncol) strip[y * SP + cc] = base[(size_t)(y + h * H) * L + cc];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 10 * h; k < 10 * h + 10; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int y = 3 * (l + 10 * k) + c - h * H;
+                x[c][k] = (colok && y >= ya && y <= yb) ? strip[y * SP + g] : make_float2(0.f, 0.f);
+            }
+        __syncthreads();
+    }
+    dft600_regs<true>(x, tile, tw2, twL, l, xrd);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        __syncthreads();  // exchange tiles / previous half's reads are done
+        if (colok) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int k = 0; k < 20; ++k)
+                    if ((10 * k + 200 * p >= H) == (h == 1))
+                        strip[(l + 10 * k + 200 * p - h * H) * SP + g] = cscale(x[p][k], scale);
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
+            const int y = idx / G, cc = idx - y * G;
+            if (cc < ncol) base[(size_t)(y + h * H) * L + cc] = strip[y * SP + cc];
+        }
+    }
+}
+
+template <int WR, int WC>
+hipError_t launch_crop600(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
+    constexpr int GC = GPW * WC;
+    const size_t lds_rows = (size_t)(L + 200 + (GPW * WR + 1) * 100) * sizeof(float2);
+    constexpr size_t strip =
+        (size_t)H * (GC + 1) > (size_t)(GC + 1) * 100 ? (size_t)H * (GC + 1) : (size_t)(GC + 1) * 100;
+    const size_t lds_cols = (L + 200 + strip) * sizeof(float2);
+    hipError_t e = hipFuncSetAttribute((const void *)k_crop_rows600<WR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds_rows);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_crop_cols600<WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_cols);
+    if (e != hipSuccess) return e;
+    if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1)
+        return hipErrorInvalidValue;
+    const int nrows = st.sy1 - st.sy0 + 1, gr = GPW * WR;
+    hipLaunchKernelGGL(k_crop_rows600<WR>, dim3((nrows + gr - 1) / gr, st.B), dim3(64 * WR), lds_rows, s,
+                       (const float2 *)st.spec, out, tw_L, st.sy0, st.sy1, st.sx0, st.sx1);
+    hipLaunchKernelGGL(k_crop_cols600<WC>, dim3((L + GC - 1) / GC, st.B), dim3(64 * WC), lds_cols, s, out, tw_L,
+                       1.0f / ((float)L * (float)L), st.sy0, st.sy1);
+    return hipGetLastError();
+}
+}  // namespace c600
+
 }  // namespace
 
 #ifndef FPM_CROP_G
@@ -234,13 +396,14 @@ hipError_t launch_crop(const DevState &st, float2 *out, const float2 *tw_L, hipS
 #define FPM_CROP_GR 4   // rows per block in the row pass
 #endif
 
-// hipErrorNotSupported when L is not 512 / 768 / 1024 (caller falls back to
+// hipErrorNotSupported when L is not 512 / 768 / 1024 / 600 (caller falls back to
 // the mixed-radix batched transform)
 hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
     switch (st.L) {
         case 512: return launch_crop<2, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
         case 768: return launch_crop<3, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
         case 1024: return launch_crop<4, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
+        case 600: return c600::launch_crop600<1, 2>(st, out, tw_L, s);
         default: return hipErrorNotSupported;
     }
 }
