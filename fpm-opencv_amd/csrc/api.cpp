@@ -39,7 +39,10 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
 size_t fused_park_elems(int nt, int B);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  float2 *pscr, int nt, unsigned long long *dbg, hipStream_t s);
+                                  float2 *pscr, int nt, unsigned long long *dbg, float2 *xch, int *flags,
+                                  hipStream_t s);
+size_t fused_xch_elems(int B);
+bool fused_split_wanted(int nt, int B, int n_cu);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
@@ -114,6 +117,8 @@ struct fpm_ctx {
                                     // g-lane groups (16: Np 256, 10: Np 200) once uploaded; 0: C-ABI
     float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
     int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
+    float2 *xch = nullptr;          // split mode (two workgroups per patch): exchange area
+    int *split_flags = nullptr;     //   handoff flags [2B] + abort flag
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
@@ -336,6 +341,13 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         c->meas_g = c->fused_mr ? 10 : 16;
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
         if ((rc = dalloc(c, &c->pscr, fused_park_elems(c->fused_nt, B)))) return fail(rc);
+        int n_cu = 0, coop = 0;
+        (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+        (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device);
+        if (c->fused_nt && coop && fused_split_wanted(c->fused_nt, B, n_cu)) {
+            if ((rc = dalloc(c, &c->xch, fused_xch_elems(B)))) return fail(rc);
+            if ((rc = dalloc(c, &c->split_flags, 2 * (size_t)B + 1))) return fail(rc);
+        }
     }
     st.meas = c->meas;
     st.disk = c->disk_dev;
@@ -530,7 +542,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->dbg,
-                                           c->stream));
+                                           c->xch, c->split_flags, c->stream));
         } else if (use_graph) {
             HIP_TRY(hipGraphLaunch(c->led_graph_exec, c->stream));
         } else {
@@ -545,6 +557,11 @@ int fpm_run(fpm_ctx *c, int iters) {
     }
     HIP_TRY(hipEventRecord(ev[need - 1], c->stream));
     HIP_TRY(hipEventSynchronize(ev[need - 1]));
+    if (c->split_flags) {  // a split-mode handoff that timed out leaves the results undefined
+        int ab = 0;
+        HIP_TRY(hipMemcpy(&ab, c->split_flags + 2 * (size_t)c->st.B, sizeof(int), hipMemcpyDeviceToHost));
+        if (ab) return set_err(FPM_ERR_DEVICE, "split-mode handoff between the two workgroups of a patch timed out");
+    }
     double led_ms = 0, crop_ms = 0;
     for (int it = 0; it < iters; ++it) {
         float a = 0, b = 0;
@@ -660,6 +677,7 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
     info->support_px = c->support_px;
     info->device = c->device;
     info->device_bytes = c->bytes;
+    info->wg_per_patch = c->xch ? 2 : 1;
     return FPM_OK;
 }
 

@@ -75,7 +75,63 @@ struct FusedArgs {
     int btx0, bty0, nbx, nbt;
     float rnbx;                 // 1 / nbx
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
+    // split mode (NT 512, B <= CUs / 2): two workgroups per patch, half h of the
+    // columns each (split_layout); handoffs through xch with device-scope flags
+    int split;
+    float2 *xch;                // [B][kXchPatch]: F partial | tail F partial | P | tail P
+    int *flags;                 // [B][2]: F partial of LED it ready (it + 1), P + spectrum of LED it (it + 1)
+    int *abort_flag;            // a handoff timed out: every workgroup leaves
 };
+
+// split-mode exchange area per patch (float2): F partials and P of the 512
+// lanes (12 slots each, lane-major) and of the <= 64 tail pixels
+constexpr int kXchF = 0, kXchTF = 12 * 512, kXchP = kXchTF + 64, kXchTP = kXchP + 12 * 512;
+constexpr int kXchPatch = kXchTP + 64;
+
+// Handoff between the two workgroups of a patch (split mode).  Everything the
+// partner reads -- the exchange area, the updated spectrum window, the flags --
+// moves with device-coherent (sc1) loads and stores (relaxed agent-scope
+// atomics), so no L2 write-back or invalidate is needed; the partner may sit
+// on another XCD.  (Agent-scope release/acquire fences instead -- buffer_wbl2 /
+// buffer_inv on every handoff -- measured 3.4x slower: they flush and
+// invalidate the whole XCD L2 that the other patches' streams use.)
+//   publish: every wave waits for its own stores to be acknowledged, then one
+//            thread stores the flag.
+//   wait:    one thread polls the flag (s_sleep between polls) and gives up
+//            after ~1 s, raising abort_flag so the partner leaves too.
+__device__ __forceinline__ void st_coh(float2 *p, float2 v) {
+    __hip_atomic_store((unsigned long long *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld_coh(const float2 *p) {
+    return __builtin_bit_cast(float2, __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void handoff_publish(int *flag, int value) {
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's coherent stores are acknowledged
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool handoff_wait(int *flag, int value, int *abort_flag, int *okslot) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (int spins = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < value; ++spins) {
+            if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                ok = 0;
+                break;
+            }
+            if (spins > (1 << 23)) {
+                __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        *okslot = ok;
+    }
+    __syncthreads();
+    return *okslot != 0;
+}
 
 // measurement stream: read once per LED, so load it non-temporally and keep
 // L2 for the spectrum window the next LED re-reads
@@ -130,14 +186,23 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     int *tky = (int *)(tpx + MAXTAIL);              // MAXTAILROWS tail rows
     float *tmx = (float *)(tky + MAXTAILROWS);      // nbt: max|spec| per band tile (upper bound if dirty)
     unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits: tile max may be stale-high
-    int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // pass-B column-block counter
+    int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // [0] pass-B column-block counter, [1] handoff result
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
     // exchange read base (see exchange16 / xchg)
     const int xrd = HALF ? opaque_int((t & 7) * XP) : exch_rbase(t);
     const int lane = tid & 63, w = tid >> 6;
-    const int b = blockIdx.x;
+    // split mode: block k -> patch 8 (k / 16) + k % 8, half (k / 8) % 2, so the two
+    // halves of a patch are 8 blocks apart (the same XCD under round-robin
+    // dispatch; only a speed matter, the handoff does not assume it)
+    const bool split = !PARK && a.split;
+    const int hown = split ? (int)((blockIdx.x >> 3) & 1) : -1;
+    const int b = split ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7)) : (int)blockIdx.x;
+    if (b >= st.B) return;  // split grid rounded up to 16 blocks (block-uniform)
+    const int hb = hown < 0 ? 0 : hown, he = hown < 0 ? 2 : hown + 1;  // halves this workgroup runs
+    float2 *xch = split ? a.xch + (size_t)b * kXchPatch : nullptr;
+    int *flg = split ? a.flags + 2 * b : nullptr;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * C::XT;
     const int nwords = (a.nbt + 31) >> 5;
@@ -278,8 +343,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 
         float2 v[16], r[16];
         float2 F[RPG][6];  // row-DFT outputs; complete after the second half
+        bool aborted = false;
 #pragma unroll 1
-        for (int h = 0; h < 2; ++h) {
+        for (int h = hb; h < he; ++h) {
             // this lane's four-step twiddles W256^{m t}, m = 0..15 (Tw)
             Tw<!PARK> wt;
             wt.load(tw2, t);
@@ -458,7 +524,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     for (int m = 0; m < 8; ++m) v[8 + m] = row[16 * m];
                     dft256_inhalf_out6<HALF, 1>(v, o, scr, wt, t, xrd);
 #pragma unroll
-                    for (int s = 0; s < 6; ++s) F[j][s] = cadd(PARK ? parkF(j, s) : F[j][s], o[s]);
+                    for (int s = 0; s < 6; ++s)
+                        F[j][s] = h == hb ? o[s] : cadd(PARK ? parkF(j, s) : F[j][s], o[s]);
                 }
             }
             if (PARK && h == 0) {  // F is not held through the second half's passes A and B
@@ -488,10 +555,46 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     s2.x += __shfl_xor(s2.x, o, 64);
                     s2.y += __shfl_xor(s2.y, o, 64);
                 }
-                if (t == 0) tailF[pp] = h ? cadd(tailF[pp], s2) : s2;
+                if (t == 0) tailF[pp] = h != hb ? cadd(tailF[pp], s2) : s2;
             }
             __syncthreads();  // half-T reusable; tailF
             FPM_STAMP(3)
+        }
+        if (split && hown == 1) {
+            // second half's workgroup: hand its F partials to the first, then wait
+            // for the updated spectrum and pupil of this LED before the next one
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) st_coh(&xch[kXchF + (j * 6 + s) * NT + tid], F[j][s]);
+            if (tid < a.n_tail_px) st_coh(&xch[kXchTF + tid], tailF[tid]);
+            handoff_publish(flg, it + 1);
+            if (it + 1 >= a.n_order) break;
+            if (!handoff_wait(flg + 1, it + 1, a.abort_flag, ccnt + 1)) break;
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) P[j][s] = ld_coh(&xch[kXchP + (j * 6 + s) * NT + tid]);
+            if (towner) Pt = ld_coh(&xch[kXchTP + tid]);
+            const float2 *sr = window(it + 1);  // written by the partner: coherent loads
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s)
+                    Opre[j][s] = ((inmask[j] >> s) & 1) ? ld_coh(sr + (kyr[j] * L + t) + soff(s)) : make_float2(0.f, 0.f);
+            if (towner) Ot = ld_coh(sr + tp.x * L + tp.y);
+            continue;
+        }
+        if (split) {  // first half's workgroup: add the second half's F partials
+            if (!handoff_wait(flg, it + 1, a.abort_flag, ccnt + 1)) {
+                aborted = true;
+                break;
+            }
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], ld_coh(&xch[kXchF + (j * 6 + s) * NT + tid]));
+            if (tid < a.n_tail_px) tailF[tid] = cadd(tailF[tid], ld_coh(&xch[kXchTF + tid]));
         }
 
         // ---- object update on the support (:405-447) and pupil numerator (:457-464).
@@ -524,7 +627,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 // this group's own half-T row is no longer read: park the numerator there
                 th[(g + NG * j) * TLD + s * 16 + t] = num;
                 if ((inmask[j] >> s) & 1) {
-                    (srow + (kyr[j] * L + t))[soff(s)] = nv;
+                    float2 *dst = srow + (kyr[j] * L + t) + soff(s);
+                    if (split) st_coh(dst, nv);  // read by the partner workgroup
+                    else *dst = nv;
                     note(yc + kyr[j], xc + kx, oa, cmag(nv));
                 }
             }
@@ -533,7 +638,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             // and the slot helper recomputes O*P the same way the gather did
             float oa;
             const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
-            srow[tp.x * L + tp.y] = nv;
+            if (split) st_coh(srow + tp.x * L + tp.y, nv);
+            else srow[tp.x * L + tp.y] = nv;
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
         FPM_STAMP(9)
@@ -627,12 +733,23 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
         for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
         pm = sqrtf(pm2);
+        if (split && it + 1 < a.n_order) {  // spectrum (written above) and P for the partner
+#pragma unroll
+            for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) st_coh(&xch[kXchP + (j * 6 + s) * NT + tid], P[j][s]);
+            if (towner) st_coh(&xch[kXchTP + tid], Pt);
+            handoff_publish(flg + 1, it + 1);
+        }
         FPM_STAMP(6)
+        (void)aborted;
     }
 #undef FPM_STAMP
+    if (hown == 1) return;  // the first half's workgroup owns the per-patch state
     // stamps of the first and the last wave (the barrier waits show who is slow)
-    if (a.dbg && (tid == 0 || tid == NT - 64))
-        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
+    // (split mode: the first wave of each half's workgroup)
+    if (a.dbg && (split ? tid == 0 : (tid == 0 || tid == NT - 64)))
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[((split ? hown : tid) ? kStamps : 0) + i], acc[i]);
 
     // ---- write back the per-patch state
     loadP();
@@ -686,7 +803,7 @@ size_t fused_lds_bytes(int nt, int nbt, int n_tail_rows) {
     const int ng = nt / 16, xt = nt > 512 ? 8 * XP : XTILE;
     return (size_t)(ng * xt + (fz::NROWS + n_tail_rows + 2) * TLD + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
-           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + sizeof(int);
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
 
 struct Band {
@@ -725,9 +842,22 @@ size_t fused_park_elems(int nt, int B) { return nt > 512 ? (size_t)B * 2 * 6 * (
 
 size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
+// split mode (two workgroups per patch): exchange-area elements for B patches
+size_t fused_xch_elems(int B) { return (size_t)B * kXchPatch; }
+
+// Split mode pays off when one workgroup per patch would leave at least half
+// of the CUs idle (BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU)
+// and needs every block co-resident (the halves wait on each other), which the
+// cooperative launch guarantees or refuses.  FPM_NO_SPLIT=1 disables it.
+bool fused_split_wanted(int nt, int B, int n_cu) {
+    if (nt != 512 || B < 1 || getenv("FPM_NO_SPLIT")) return false;
+    return 16 * ((B + 7) / 8) <= n_cu;
+}
+
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  float2 *pscr, int nt, unsigned long long *dbg, hipStream_t s) {
+                                  float2 *pscr, int nt, unsigned long long *dbg, float2 *xch, int *flags,
+                                  hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
     if (!g.ok || (nt != 512 && nt != 1024)) return hipErrorInvalidValue;
     if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
@@ -765,11 +895,23 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.nbt = bd.nbt;
     a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
+    a.split = xch != nullptr;
+    a.xch = xch;
+    a.flags = flags;
+    a.abort_flag = flags ? flags + 2 * st.B : nullptr;
     const size_t lds = fused_lds_bytes(nt, a.nbt, g.n_tail_rows);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024> : (const void *)k_fused_iteration<512>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    if (a.split) {
+        if (nt != 512) return hipErrorInvalidValue;
+        // flags count LEDs of this launch: start from zero (and no abort)
+        e = hipMemsetAsync(flags, 0, (2 * (size_t)st.B + 1) * sizeof(int), s);
+        if (e != hipSuccess) return e;
+        void *args[] = {&a};
+        return hipLaunchCooperativeKernel(fn, dim3(16 * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
+    }
     if (nt == 1024)
         hipLaunchKernelGGL(k_fused_iteration<1024>, dim3(st.B), dim3(1024), lds, s, a);
     else

@@ -74,7 +74,7 @@ class fpm_frames(C.Structure):
 
 class fpm_info(C.Structure):
     _fields_ = [("path", C.c_int32), ("box", C.c_int32), ("support_px", C.c_int32),
-                ("device", C.c_int32), ("device_bytes", C.c_size_t)]
+                ("device", C.c_int32), ("device_bytes", C.c_size_t), ("wg_per_patch", C.c_int32)]
 
 
 class fpm_timing(C.Structure):

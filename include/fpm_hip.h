@@ -122,6 +122,8 @@ typedef struct fpm_info {
     int32_t support_px;    /* pixels in the pupil support disk                  */
     int32_t device;
     size_t  device_bytes;  /* device memory owned by the context               */
+    int32_t wg_per_patch;  /* fused Np 256 path: 2 when each patch is split over
+                              two workgroups (n_patch <= CUs / 2), else 1       */
 } fpm_info;
 
 /* Per-kernel timing of the most recent fpm_run, from HIP events recorded on
