@@ -346,7 +346,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device);
         if (c->fused_nt && coop && fused_split_wanted(c->fused_nt, B, n_cu)) {
             if ((rc = dalloc(c, &c->xch, fused_xch_elems(B)))) return fail(rc);
-            if ((rc = dalloc(c, &c->split_flags, 2 * (size_t)B + 1))) return fail(rc);
+            if ((rc = dalloc(c, &c->split_flags, 4 * (size_t)B + 1))) return fail(rc);
         }
     }
     st.meas = c->meas;

@@ -79,7 +79,8 @@ struct FusedArgs {
     // columns each (split_layout); handoffs through xch with device-scope flags
     int split;
     float2 *xch;                // [B][kXchPatch]: F partial | tail F partial | P | tail P
-    int *flags;                 // [B][2]: F partial of LED it ready (it + 1), P + spectrum of LED it (it + 1)
+    int *flags;                 // [B][2]: F partial of LED it ready (it + 1), P + spectrum of LED it (it + 1);
+                                // then the abort flag, then [B][2] XCC_ID + 1 of each half
     int *abort_flag;            // a handoff timed out: every workgroup leaves
 };
 
@@ -107,15 +108,42 @@ __device__ __forceinline__ float2 ld_coh(const float2 *p) {
     return __builtin_bit_cast(float2, __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT));
 }
-__device__ __forceinline__ void handoff_publish(int *flag, int value) {
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's coherent stores are acknowledged
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Co-located pair (both workgroups report the same XCC_ID): the XCD's L2 is
+// the coherence point, so stores stay plain (the L1 writes through) and loads
+// bypass the L1 only (sc0 buffer loads): L2 round trips instead of memory
+// round trips on the critical path between the two halves.
+// aux: bit 0 = sc0 (bypass the L1), bit 31 = volatile (keeps the compiler from
+// hoisting a polled load out of its loop or merging it with earlier reads)
+constexpr int kAuxL2Volatile = (int)(1u | (1u << 31));
+__device__ __forceinline__ float2 ld_l2(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, kAuxL2Volatile));
 }
-__device__ __forceinline__ bool handoff_wait(int *flag, int value, int *abort_flag, int *okslot) {
+__device__ __forceinline__ int ld_l2_i32(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, kAuxL2Volatile);
+}
+__device__ __forceinline__ int xcc_id() {
+    int x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 15;
+}
+__device__ __forceinline__ void handoff_publish(int *flag, int value, bool local) {
+#ifndef FPM_EXP_NOWAIT  // timing experiment only (racy)
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are acknowledged
+#endif
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (local) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__device__ __forceinline__ bool handoff_wait(int *flag, int value, int *abort_flag, int *okslot, bool local,
+                                             __amdgpu_buffer_rsrc_t rflag, int flag_off) {
     if (threadIdx.x == 0) {
         int ok = 1;
-        for (int spins = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < value; ++spins) {
+        for (int spins = 0;
+             (local ? ld_l2_i32(rflag, flag_off) : __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
+             value;
+             ++spins) {
             if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 ok = 0;
                 break;
@@ -203,6 +231,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     const int hb = hown < 0 ? 0 : hown, he = hown < 0 ? 2 : hown + 1;  // halves this workgroup runs
     float2 *xch = split ? a.xch + (size_t)b * kXchPatch : nullptr;
     int *flg = split ? a.flags + 2 * b : nullptr;
+    int *xccs = split ? a.flags + 2 * st.B + 1 + 2 * b : nullptr;  // [2]: XCC_ID + 1 of each half
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * C::XT;
     const int nwords = (a.nbt + 31) >> 5;
@@ -292,6 +321,45 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
     float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
     float pm = st.pmax[b];
+    // split mode: learn whether the partner shares this XCD (then L2-level
+    // handoffs, see ld_l2) -- one coherent exchange per launch
+    bool local = false;
+    // (descriptors are built unconditionally: the type has no empty state)
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(xch, 0, split ? kXchPatch * (int)sizeof(float2) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(spec, 0, split ? L * L * (int)sizeof(float2) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, split ? 2 * (int)sizeof(int) : 0, 0x00020000);
+    if (split) {
+        if (tid == 0) {
+            const int mine = xcc_id() + 1;
+            __hip_atomic_store(xccs + hown, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int other = 0;
+            for (int spins = 0; (other = __hip_atomic_load(xccs + 1 - hown, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)) == 0; ++spins) {
+                if (spins > (1 << 23) || __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            ccnt[1] = other == mine;
+        }
+        __syncthreads();
+        local = ccnt[1] != 0;
+        __syncthreads();  // ccnt[1] is reused by handoff_wait
+    }
+    // exchange-area and partner-visible spectrum accesses of split mode
+    auto xst = [&](int idx, float2 v) {
+        if (local) xch[idx] = v;
+        else st_coh(&xch[idx], v);
+    };
+    auto xld = [&](int idx) { return local ? ld_l2(rx, idx * (int)sizeof(float2)) : ld_coh(&xch[idx]); };
+    auto sst = [&](float2 *p, float2 v) {
+        if (!split || local) *p = v;
+        else st_coh(p, v);
+    };
+    auto sld = [&](const float2 *p) {
+        return local ? ld_l2(rs, (int)(p - spec) * (int)sizeof(float2)) : ld_coh(p);
+    };
     const float epsn = st.eps * (float)(NP * NP);  // eps on the unscaled IDFT
     const float epsn_im = st.eps_im * (float)(NP * NP);
     __syncthreads();
@@ -566,35 +634,37 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) st_coh(&xch[kXchF + (j * 6 + s) * NT + tid], F[j][s]);
-            if (tid < a.n_tail_px) st_coh(&xch[kXchTF + tid], tailF[tid]);
-            handoff_publish(flg, it + 1);
+                for (int s = 0; s < 6; ++s) xst(kXchF + (j * 6 + s) * NT + tid, F[j][s]);
+            if (tid < a.n_tail_px) xst(kXchTF + tid, tailF[tid]);
+            handoff_publish(flg, it + 1, local);
+            FPM_STAMP(9)  // (split, second half: the publish)
             if (it + 1 >= a.n_order) break;
-            if (!handoff_wait(flg + 1, it + 1, a.abort_flag, ccnt + 1)) break;
+            if (!handoff_wait(flg + 1, it + 1, a.abort_flag, ccnt + 1, local, rf, (int)sizeof(int))) break;
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) P[j][s] = ld_coh(&xch[kXchP + (j * 6 + s) * NT + tid]);
-            if (towner) Pt = ld_coh(&xch[kXchTP + tid]);
+                for (int s = 0; s < 6; ++s) P[j][s] = xld(kXchP + (j * 6 + s) * NT + tid);
+            if (towner) Pt = xld(kXchTP + tid);
             const float2 *sr = window(it + 1);  // written by the partner: coherent loads
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
                 for (int s = 0; s < 6; ++s)
-                    Opre[j][s] = ((inmask[j] >> s) & 1) ? ld_coh(sr + (kyr[j] * L + t) + soff(s)) : make_float2(0.f, 0.f);
-            if (towner) Ot = ld_coh(sr + tp.x * L + tp.y);
+                    Opre[j][s] = ((inmask[j] >> s) & 1) ? sld(sr + (kyr[j] * L + t) + soff(s)) : make_float2(0.f, 0.f);
+            if (towner) Ot = sld(sr + tp.x * L + tp.y);
+            FPM_STAMP(4)  // (split, second half: the wait for the partner and the reloads)
             continue;
         }
         if (split) {  // first half's workgroup: add the second half's F partials
-            if (!handoff_wait(flg, it + 1, a.abort_flag, ccnt + 1)) {
+            if (!handoff_wait(flg, it + 1, a.abort_flag, ccnt + 1, local, rf, 0)) {
                 aborted = true;
                 break;
             }
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], ld_coh(&xch[kXchF + (j * 6 + s) * NT + tid]));
-            if (tid < a.n_tail_px) tailF[tid] = cadd(tailF[tid], ld_coh(&xch[kXchTF + tid]));
+                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], xld(kXchF + (j * 6 + s) * NT + tid));
+            if (tid < a.n_tail_px) tailF[tid] = cadd(tailF[tid], xld(kXchTF + tid));
         }
 
         // ---- object update on the support (:405-447) and pupil numerator (:457-464).
@@ -627,9 +697,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 // this group's own half-T row is no longer read: park the numerator there
                 th[(g + NG * j) * TLD + s * 16 + t] = num;
                 if ((inmask[j] >> s) & 1) {
-                    float2 *dst = srow + (kyr[j] * L + t) + soff(s);
-                    if (split) st_coh(dst, nv);  // read by the partner workgroup
-                    else *dst = nv;
+                    sst(srow + (kyr[j] * L + t) + soff(s), nv);  // read by a split partner
                     note(yc + kyr[j], xc + kx, oa, cmag(nv));
                 }
             }
@@ -638,8 +706,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             // and the slot helper recomputes O*P the same way the gather did
             float oa;
             const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
-            if (split) st_coh(srow + tp.x * L + tp.y, nv);
-            else srow[tp.x * L + tp.y] = nv;
+            sst(srow + tp.x * L + tp.y, nv);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
         FPM_STAMP(9)
@@ -737,19 +804,19 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) st_coh(&xch[kXchP + (j * 6 + s) * NT + tid], P[j][s]);
-            if (towner) st_coh(&xch[kXchTP + tid], Pt);
-            handoff_publish(flg + 1, it + 1);
+                for (int s = 0; s < 6; ++s) xst(kXchP + (j * 6 + s) * NT + tid, P[j][s]);
+            if (towner) xst(kXchTP + tid, Pt);
+            handoff_publish(flg + 1, it + 1, local);
         }
         FPM_STAMP(6)
         (void)aborted;
     }
 #undef FPM_STAMP
-    if (hown == 1) return;  // the first half's workgroup owns the per-patch state
     // stamps of the first and the last wave (the barrier waits show who is slow)
     // (split mode: the first wave of each half's workgroup)
     if (a.dbg && (split ? tid == 0 : (tid == 0 || tid == NT - 64)))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[((split ? hown : tid) ? kStamps : 0) + i], acc[i]);
+    if (hown == 1) return;  // the first half's workgroup owns the per-patch state
 
     // ---- write back the per-patch state
     loadP();
@@ -907,7 +974,7 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     if (a.split) {
         if (nt != 512) return hipErrorInvalidValue;
         // flags count LEDs of this launch: start from zero (and no abort)
-        e = hipMemsetAsync(flags, 0, (2 * (size_t)st.B + 1) * sizeof(int), s);
+        e = hipMemsetAsync(flags, 0, (4 * (size_t)st.B + 1) * sizeof(int), s);
         if (e != hipSuccess) return e;
         void *args[] = {&a};
         return hipLaunchCooperativeKernel(fn, dim3(16 * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
