@@ -100,14 +100,6 @@ constexpr int kXchPatch = kXchTP + 64;
 //            thread stores the flag.
 //   wait:    one thread polls the flag (s_sleep between polls) and gives up
 //            after ~1 s, raising abort_flag so the partner leaves too.
-__device__ __forceinline__ void st_coh(float2 *p, float2 v) {
-    __hip_atomic_store((unsigned long long *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float2 ld_coh(const float2 *p) {
-    return __builtin_bit_cast(float2, __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT));
-}
 // Co-located pair (both workgroups report the same XCC_ID): the XCD's L2 is
 // the coherence point, so stores stay plain (the L1 writes through) and loads
 // bypass the L1 only (sc0 buffer loads): L2 round trips instead of memory
@@ -194,7 +186,7 @@ struct FzCfg {
     static constexpr int XT = HALF ? 8 * XP : XTILE;  // exchange tile per group (complex)
 };
 
-template <int NT>
+template <int NT, bool SPLIT>
 __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     using namespace fz;
     using C = FzCfg<NT>;
@@ -224,7 +216,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     // split mode: block k -> patch 8 (k / 16) + k % 8, half (k / 8) % 2, so the two
     // halves of a patch are 8 blocks apart (the same XCD under round-robin
     // dispatch; only a speed matter, the handoff does not assume it)
-    const bool split = !PARK && a.split;
+    constexpr bool split = SPLIT && !PARK;  // a separate instance: the one-workgroup kernel carries no split state
     const int hown = split ? (int)((blockIdx.x >> 3) & 1) : -1;
     const int b = split ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7)) : (int)blockIdx.x;
     if (b >= st.B) return;  // split grid rounded up to 16 blocks (block-uniform)
@@ -348,17 +340,37 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         __syncthreads();  // ccnt[1] is reused by handoff_wait
     }
     // exchange-area and partner-visible spectrum accesses of split mode
-    auto xst = [&](int idx, float2 v) {
-        if (local) xch[idx] = v;
-        else st_coh(&xch[idx], v);
+    // Exchange-area accesses go through buffer instructions: one per-lane VGPR
+    // offset (the lane's 8-byte slot) plus the slot's compile-time byte offset
+    // in the SGPR soffset, so no 64-bit address per slot is kept live (with
+    // plain pointers the 13 P stores had their addresses spilled to scratch,
+    // each store paying a reload and a vmcnt(0): 9k cycles per LED).
+    // cache policy: sc1 (16) when the partner is on another XCD; loads are
+    // volatile (bit 31) and bypass the L1 (sc0) when it shares this one.
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    const int lane_off = tid * (int)sizeof(float2);
+    auto xst = [&](int slot, float2 v) {  // slot: the lane-independent part of the index
+        const u32x2_t d = __builtin_bit_cast(u32x2_t, v);
+        if (local) __builtin_amdgcn_raw_buffer_store_b64(d, rx, lane_off, slot * (int)sizeof(float2), 0);
+        else __builtin_amdgcn_raw_buffer_store_b64(d, rx, lane_off, slot * (int)sizeof(float2), 16);
     };
-    auto xld = [&](int idx) { return local ? ld_l2(rx, idx * (int)sizeof(float2)) : ld_coh(&xch[idx]); };
+    auto xld = [&](int slot) {
+        return __builtin_bit_cast(
+            float2, local ? __builtin_amdgcn_raw_buffer_load_b64(rx, lane_off, slot * (int)sizeof(float2), kAuxL2Volatile)
+                          : __builtin_amdgcn_raw_buffer_load_b64(rx, lane_off, slot * (int)sizeof(float2),
+                                                                 (int)(16u | (1u << 31))));
+    };
     auto sst = [&](float2 *p, float2 v) {
         if (!split || local) *p = v;
-        else st_coh(p, v);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
+                                                  (int)(p - spec) * (int)sizeof(float2), 0, 16);
     };
     auto sld = [&](const float2 *p) {
-        return local ? ld_l2(rs, (int)(p - spec) * (int)sizeof(float2)) : ld_coh(p);
+        const int off = (int)(p - spec) * (int)sizeof(float2);
+        return __builtin_bit_cast(float2, local ? __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, kAuxL2Volatile)
+                                                : __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0,
+                                                                                       (int)(16u | (1u << 31))));
     };
     const float epsn = st.eps * (float)(NP * NP);  // eps on the unscaled IDFT
     const float epsn_im = st.eps_im * (float)(NP * NP);
@@ -634,8 +646,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) xst(kXchF + (j * 6 + s) * NT + tid, F[j][s]);
-            if (tid < a.n_tail_px) xst(kXchTF + tid, tailF[tid]);
+                for (int s = 0; s < 6; ++s) xst(kXchF + (j * 6 + s) * NT, F[j][s]);
+            if (tid < a.n_tail_px) xst(kXchTF, tailF[tid]);
             handoff_publish(flg, it + 1, local);
             FPM_STAMP(9)  // (split, second half: the publish)
             if (it + 1 >= a.n_order) break;
@@ -643,8 +655,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) P[j][s] = xld(kXchP + (j * 6 + s) * NT + tid);
-            if (towner) Pt = xld(kXchTP + tid);
+                for (int s = 0; s < 6; ++s) P[j][s] = xld(kXchP + (j * 6 + s) * NT);
+            if (towner) Pt = xld(kXchTP);
             const float2 *sr = window(it + 1);  // written by the partner: coherent loads
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
@@ -663,8 +675,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], xld(kXchF + (j * 6 + s) * NT + tid));
-            if (tid < a.n_tail_px) tailF[tid] = cadd(tailF[tid], xld(kXchTF + tid));
+                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], xld(kXchF + (j * 6 + s) * NT));
+            if (tid < a.n_tail_px) tailF[tid] = cadd(tailF[tid], xld(kXchTF));
         }
 
         // ---- object update on the support (:405-447) and pupil numerator (:457-464).
@@ -800,15 +812,17 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
         for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
         pm = sqrtf(pm2);
+        FPM_STAMP(6)
         if (split && it + 1 < a.n_order) {  // spectrum (written above) and P for the partner
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) xst(kXchP + (j * 6 + s) * NT + tid, P[j][s]);
-            if (towner) xst(kXchTP + tid, Pt);
+                for (int s = 0; s < 6; ++s) xst(kXchP + (j * 6 + s) * NT, P[j][s]);
+            if (towner) xst(kXchTP, Pt);
+            FPM_STAMP(11)
             handoff_publish(flg + 1, it + 1, local);
+            FPM_STAMP(12)
         }
-        FPM_STAMP(6)
         (void)aborted;
     }
 #undef FPM_STAMP
@@ -968,7 +982,9 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.abort_flag = flags ? flags + 2 * st.B : nullptr;
     const size_t lds = fused_lds_bytes(nt, a.nbt, g.n_tail_rows);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024> : (const void *)k_fused_iteration<512>;
+    const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024, false>
+                     : a.split  ? (const void *)k_fused_iteration<512, true>
+                                : (const void *)k_fused_iteration<512, false>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (a.split) {
@@ -980,9 +996,9 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
         return hipLaunchCooperativeKernel(fn, dim3(16 * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
     }
     if (nt == 1024)
-        hipLaunchKernelGGL(k_fused_iteration<1024>, dim3(st.B), dim3(1024), lds, s, a);
+        hipLaunchKernelGGL((k_fused_iteration<1024, false>), dim3(st.B), dim3(1024), lds, s, a);
     else
-        hipLaunchKernelGGL(k_fused_iteration<512>, dim3(st.B), dim3(512), lds, s, a);
+        hipLaunchKernelGGL((k_fused_iteration<512, false>), dim3(st.B), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 

@@ -35,7 +35,7 @@
 namespace fpm {
 
 constexpr int kTile = 16;
-constexpr int kStamps = 11;  // FPM_STAMPS phase counters of the fused kernel (per recorded wave)
+constexpr int kStamps = 13;  // FPM_STAMPS phase counters of the fused kernel (per recorded wave)
 
 struct DevState {
     float2 *spec;
