@@ -57,6 +57,8 @@ WORKLOADS = {
           "one runFPM iteration per step",
     "c5": "config 5: Np=1024, L=4096 spectrum in fp16, naRadius 333, 512-LED synthetic grid, "
           "one runFPM iteration per step",
+    "c2": "config 2: dataset_mono.json with the dome fallback (Np=90, L=360, naRadius 30, 193 LEDs), "
+          "64 patches, one runFPM iteration per step",
 }
 
 
@@ -65,6 +67,8 @@ def config_geometry(name, np_=256):
       metric  configs[1]-style headline: dogStomach optics, Np 256, 293 LEDs
       c3      configs[2] literal dataset_dogStomach.json: Np 200, maxNA 0.4 ->
               L 600, naRadius 26, 157 LEDs (general path, mixed radix)
+      c2      configs[1]: dataset_mono.json + dome fallback (the config-1
+              geometry: Np 90, L 360, r 30, 193 LEDs), 64 patches (general path)
       c5      configs[4]: Np 1024, L 4096, naRadius 333 (mono optics at
               Np 1024), 512 LEDs of a synthetic square grid
               (23 x 23 at a 128-px k-space pitch, the 512 nearest the centre),
@@ -75,6 +79,11 @@ def config_geometry(name, np_=256):
         return metric_geometry(np_)
     if name == "c3":
         return metric_geometry(200, max_na=0.4)
+    if name == "c2":
+        import numpy as np
+        g = config1_geometry()
+        g["order_leds"] = np.arange(g["n_led"])
+        return g
     if name == "c5":
         import numpy as np
         from tools.synth import grid_geometry
@@ -222,12 +231,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--patches", type=int, default=0, help="patches per GPU (0: 256, 8 for --config c5)")
+    ap.add_argument("--patches", type=int, default=0, help="patches per GPU (0: 256, 8 for --config c5, 64 for c2)")
     ap.add_argument("--patches-total", type=int, default=0,
                     help="strong scaling: one field of T patches sharded over the ranks (parallel.shard_range), "
                          "gathered and stitched on rank 0 after the timed region; 0 = weak scaling (--patches per rank)")
     ap.add_argument("--np", type=int, default=256)
-    ap.add_argument("--config", default="metric", choices=["metric", "c3", "c5"],
+    ap.add_argument("--config", default="metric", choices=["metric", "c2", "c3", "c5"],
                     help="workload (config_geometry); only 'metric' is the headline line")
     ap.add_argument("--fp16", action="store_true", help="fp16 spectrum storage (default for --config c5)")
     ap.add_argument("--path", default="auto", choices=["auto", "general", "fused"])
@@ -277,7 +286,7 @@ def main():
         if B < 1:
             raise SystemExit(f"rank {rank}: empty shard of {args.patches_total} patches over {world} ranks")
     else:
-        B = args.patches if args.patches > 0 else (8 if args.config == "c5" else 256)
+        B = args.patches if args.patches > 0 else {"c5": 8, "c2": 64}.get(args.config, 256)
         seed, poff = 20261015 + 1000 * rank, 0
     if args.data == "random":
         g = torch.Generator(device="cuda")

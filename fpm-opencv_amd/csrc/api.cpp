@@ -36,6 +36,11 @@ bool fused_mr_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                      const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                      unsigned long long *dbg, hipStream_t s);
+// small-patch fused kernel (fused_small.hip, Np <= 96)
+bool fused_small_supported(int np, int r, const DevState &st);
+hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
+                                        const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
+                                        const FftPlan &pl, hipStream_t s);
 size_t fused_park_elems(int nt, int B);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
@@ -120,6 +125,7 @@ struct fpm_ctx {
     float2 *xch = nullptr;          // split mode (two workgroups per patch): exchange area
     int *split_flags = nullptr;     //   handoff flags [2B] + abort flag
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
+    bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -303,7 +309,8 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     const bool fp16 = (prob->flags & FPM_FLAG_SPEC_FP16) != 0;
     c->fused_nt = fused_threads(np, r, L, st);
     c->fused_mr = !c->fused_nt && fused_mr_supported(np, r, st);
-    const bool fused_ok = c->fused_nt || c->fused_mr;
+    c->fused_small = !c->fused_nt && !c->fused_mr && !getenv("FPM_NO_SMALL") && fused_small_supported(np, r, st);
+    const bool fused_ok = c->fused_nt || c->fused_mr || c->fused_small;
     if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_ok))
         return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
                             fp16 ? " with fp16 spectrum storage" : ""));
@@ -338,7 +345,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
     } else {
-        c->meas_g = c->fused_mr ? 10 : 16;
+        c->meas_g = c->fused_small ? np : c->fused_mr ? 10 : 16;
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
         if ((rc = dalloc(c, &c->pscr, fused_park_elems(c->fused_nt, B)))) return fail(rc);
         int n_cu = 0, coop = 0;
@@ -536,7 +543,10 @@ int fpm_run(fpm_ctx *c, int iters) {
     HIP_TRY(hipEventRecord(ev[0], c->stream));
     for (int it = 0; it < iters; ++it) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
-        if (c->path == FPM_PATH_FUSED && c->fused_mr) {
+        if (c->path == FPM_PATH_FUSED && c->fused_small) {
+            HIP_TRY(launch_fused_small_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
+                                                 c->prob.n_order, c->tw_np, c->pl_np, c->stream));
+        } else if (c->path == FPM_PATH_FUSED && c->fused_mr) {
             HIP_TRY(launch_fused_mr_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED) {

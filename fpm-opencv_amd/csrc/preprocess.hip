@@ -129,12 +129,36 @@ hipError_t launch_layout(uint16_t *meas, size_t nimg, bool fwd, hipStream_t s) {
         hipLaunchKernelGGL((k_meas_layout<NP, G, false>), dim3((unsigned)nimg), dim3(1024), lds, s, meas, nimg);
     return hipGetLastError();
 }
+// g = Np (small-patch fused kernel, any Np <= 128): the plain transpose
+// stored[x Np + y] = I[y][x], its own inverse
+__global__ void __launch_bounds__(1024) k_meas_transpose(uint16_t *meas, int np, size_t nimg) {
+    extern __shared__ uint16_t tl[];  // np x (np + 2)
+    const int ld = np + 2, nn = np * np;
+    const size_t img = blockIdx.x;
+    if (img >= nimg) return;
+    uint16_t *p = meas + img * nn;
+    for (int i = threadIdx.x; i < nn; i += 1024) {
+        const int a = i / np, b = i - a * np;
+        tl[a * ld + b] = p[i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nn; i += 1024) {
+        const int a = i / np, b = i - a * np;
+        p[i] = tl[b * ld + a];
+    }
+}
 }  // namespace
 
-// g = 16 (Np 256 fused kernel) or 10 (Np 200 fused kernel)
+// g = 16 (Np 256 fused kernel), 10 (Np 200 fused kernel) or Np (small-patch kernel)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s) {
     if (np == 256 && g == 16) return launch_layout<256, 16>(meas, nimg, fwd, s);
     if (np == 200 && g == 10) return launch_layout<200, 10>(meas, nimg, fwd, s);
+    if (g == np && np <= 128) {
+        if (nimg == 0) return hipSuccess;
+        const size_t lds = (size_t)np * (np + 2) * sizeof(uint16_t);
+        hipLaunchKernelGGL(k_meas_transpose, dim3((unsigned)nimg), dim3(1024), lds, s, meas, np, nimg);
+        return hipGetLastError();
+    }
     return hipErrorInvalidValue;
 }
 
