@@ -41,6 +41,8 @@ bool fused_small_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                         const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                         const FftPlan &pl, hipStream_t s);
+// Np 1024 register row/column kernels of the general path (np1024.hip)
+bool np1024_supported(int np, int r);
 size_t fused_park_elems(int nt, int B);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
@@ -118,8 +120,9 @@ struct fpm_ctx {
     float2 *tw_np = nullptr, *tw_L = nullptr;
     float2 *objcrop = nullptr;
     uint16_t *meas = nullptr;
-    int meas_g = 0;                 // fused paths: meas holds the column layout of meas_layout with
-                                    // g-lane groups (16: Np 256, 10: Np 200) once uploaded; 0: C-ABI
+    int meas_g = 0;                 // meas holds the column layout of meas_layout with g-lane groups
+                                    // once uploaded (16: Np 256, 10: Np 200, Np: the small-patch
+                                    // kernel and the Np 1024 general path, transposed); 0: C-ABI
     float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
     int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
     float2 *xch = nullptr;          // split mode (two workgroups per patch): exchange area
@@ -341,6 +344,8 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &c->x0_dev, (size_t)prob->n_stack))) return fail(rc);
     if ((rc = dalloc(c, &c->y0_dev, (size_t)prob->n_stack))) return fail(rc);
     if (c->path == FPM_PATH_GENERAL) {
+        // Np 1024: register-resident row/column kernels reading the stack transposed
+        if (np1024_supported(np, r) && !getenv("FPM_NO_REG1024")) c->meas_g = np;
         if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);

@@ -37,6 +37,12 @@ namespace fpm {
 constexpr int kTile = 16;
 constexpr int kStamps = 13;  // FPM_STAMPS phase counters of the fused kernel (per recorded wave)
 
+// one LED step of the general path (general.hip, np1024.hip)
+struct StepArgs {
+    int xc, yc;      // centre of the sub-aperture in the centred spectrum
+    int led;         // stack index
+};
+
 struct DevState {
     float2 *spec;
     __half2 *spec16;  // fp16 storage of the spectrum (spec == nullptr then)

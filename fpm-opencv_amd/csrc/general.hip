@@ -29,11 +29,6 @@
 
 namespace fpm {
 
-struct StepArgs {
-    int xc, yc;      // centre of the sub-aperture in the centred spectrum
-    int led;         // stack index
-};
-
 // ---- K1 ---------------------------------------------------------------------
 // grid (nb, B), block 256, LDS 2*Np float2
 __global__ void __launch_bounds__(256) k_gather_rowifft(DevState st, StepArgs sa, FftPlan pl,
@@ -792,73 +787,81 @@ static bool fft_fits(const FftPlan &pl, int lc, int nt = kFftThreads, int e = kF
     return true;
 }
 
+hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, hipStream_t s);
+
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
                                const float2 *tw, hipStream_t s) {
     StepArgs sa;
     sa.led = led;
     sa.xc = x0 + st.np / 2;
     sa.yc = y0 + st.np / 2;
-    const size_t lds = 2 * (size_t)st.np * sizeof(float2);
-    // row kernels: up to 16 box rows per block, fewer while a few large
-    // patches would leave the chip short of blocks (one row per block when
-    // not even 2 rows fit a 256-thread tile)
-    int lr = 4;
-    while (lr > 0 && !fft_fits(pl, lr, 256)) --lr;
-    auto rblk = [&](int l) { return ((st.nb + (1 << l) - 1) >> l) * st.B; };
-    while (lr > 1 && rblk(lr) < 512) --lr;
-    const size_t ldr = ((size_t)row_pitch(st.np, lr) * (1 << lr) + st.np) * sizeof(float2);
-    const dim3 rgrid((st.nb + (1 << lr) - 1) >> lr, st.B);
-    // 16 register elements per thread when the tile allows (fewer VGPRs, more
-    // waves per SIMD to hide the LDS round trips of each pass), else 24
-    const bool r16 = lr > 0 && fft_fits(pl, lr, 256, 16);
-    if (lr > 0 && r16)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gather_rowifft_tiled<256, 16>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
-    else if (lr > 0)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gather_rowifft_tiled<256, 24>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
-    else
-        hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
-    // tiled column pass: up to 16 columns per block while the tile fits the
-    // in-place register-lifted transform, fewer (down to 4) when a few large
-    // patches would leave the chip short of blocks; one column per block when
-    // not even 2 columns fit
-    int lc = 4;
-    while (lc > 0 && !fft_fits(pl, lc)) --lc;
-    auto nblk = [&](int l) { return ((st.np + (1 << l) - 1) >> l) * st.B; };
-    while (lc > 2 && nblk(lc) < 512) --lc;
-    const int cw = colw_cw(pl);
-    if (cw > 1 && !std::getenv("FPM_NO_WAVE_COLS")) {
-        // wave-private columns: 4 waves x CW columns, 8 waves when a wave
-        // holds a single (long) column
-        const int P = colw_pitch(st.np);
-        const int nw = cw == 1 ? 8 : 4, C = nw * cw;
-        const size_t ldw = ((size_t)C * P + st.np) * sizeof(float2);
-        const dim3 grid((st.np + C - 1) / C, st.B);
-        if (cw == 4)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<4, 4>), grid, dim3(256), ldw, s, st, sa, pl, tw, P);
-        else if (cw == 2)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<4, 2>), grid, dim3(256), ldw, s, st, sa, pl, tw, P);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<8, 1>), grid, dim3(512), ldw, s, st, sa, pl, tw, P);
-    } else if (lc > 0) {
-        const size_t ldt = ((size_t)st.np * (1 << lc) + st.np) * sizeof(float2);
-        const dim3 grid((st.np + (1 << lc) - 1) >> lc, st.B);
-        if (fft_fits(pl, lc, 256, 16))
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<256, 16>), grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
-        else if (fft_fits(pl, lc, 256))
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<256, 24>), grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
-        else if (fft_fits(pl, lc, kFftThreads, 16))
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<kFftThreads, 16>), grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<kFftThreads, 24>), grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
+    if (st.np == 1024 && st.meas_g == 1024) {
+        // Np 1024: register-resident row/column transforms (np1024.hip)
+        const hipError_t e = launch_np1024_rows_cols(st, sa, tw, s);
+        if (e != hipSuccess) return e;
     } else {
-        hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
+        const size_t lds = 2 * (size_t)st.np * sizeof(float2);
+        // row kernels: up to 16 box rows per block, fewer while a few large
+        // patches would leave the chip short of blocks (one row per block when
+        // not even 2 rows fit a 256-thread tile)
+        int lr = 4;
+        while (lr > 0 && !fft_fits(pl, lr, 256)) --lr;
+        auto rblk = [&](int l) { return ((st.nb + (1 << l) - 1) >> l) * st.B; };
+        while (lr > 1 && rblk(lr) < 512) --lr;
+        const size_t ldr = ((size_t)row_pitch(st.np, lr) * (1 << lr) + st.np) * sizeof(float2);
+        const dim3 rgrid((st.nb + (1 << lr) - 1) >> lr, st.B);
+        // 16 register elements per thread when the tile allows (fewer VGPRs, more
+        // waves per SIMD to hide the LDS round trips of each pass), else 24
+        const bool r16 = lr > 0 && fft_fits(pl, lr, 256, 16);
+        if (lr > 0 && r16)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gather_rowifft_tiled<256, 16>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+        else if (lr > 0)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gather_rowifft_tiled<256, 24>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+        else
+            hipLaunchKernelGGL(k_gather_rowifft, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
+        // tiled column pass: up to 16 columns per block while the tile fits the
+        // in-place register-lifted transform, fewer (down to 4) when a few large
+        // patches would leave the chip short of blocks; one column per block when
+        // not even 2 columns fit
+        int lc = 4;
+        while (lc > 0 && !fft_fits(pl, lc)) --lc;
+        auto nblk = [&](int l) { return ((st.np + (1 << l) - 1) >> l) * st.B; };
+        while (lc > 2 && nblk(lc) < 512) --lc;
+        const int cw = colw_cw(pl);
+        if (cw > 1 && !std::getenv("FPM_NO_WAVE_COLS")) {
+            // wave-private columns: 4 waves x CW columns, 8 waves when a wave
+            // holds a single (long) column
+            const int P = colw_pitch(st.np);
+            const int nw = cw == 1 ? 8 : 4, C = nw * cw;
+            const size_t ldw = ((size_t)C * P + st.np) * sizeof(float2);
+            const dim3 grid((st.np + C - 1) / C, st.B);
+            if (cw == 4)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<4, 4>), grid, dim3(256), ldw, s, st, sa, pl, tw, P);
+            else if (cw == 2)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<4, 2>), grid, dim3(256), ldw, s, st, sa, pl, tw, P);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_wave<8, 1>), grid, dim3(512), ldw, s, st, sa, pl, tw, P);
+        } else if (lc > 0) {
+            const size_t ldt = ((size_t)st.np * (1 << lc) + st.np) * sizeof(float2);
+            const dim3 grid((st.np + (1 << lc) - 1) >> lc, st.B);
+            if (fft_fits(pl, lc, 256, 16))
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<256, 16>), grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
+            else if (fft_fits(pl, lc, 256))
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<256, 24>), grid, dim3(256), ldt, s, st, sa, pl, tw, lc);
+            else if (fft_fits(pl, lc, kFftThreads, 16))
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<kFftThreads, 16>), grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_colpass_tiled<kFftThreads, 24>), grid, dim3(kFftThreads), ldt, s, st, sa, pl, tw, lc);
+        } else {
+            hipLaunchKernelGGL(k_colpass, dim3(st.np, st.B), dim3(256), lds, s, st, sa, pl, tw);
+        }
+        if (lr > 0 && r16)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rowfft_update_tiled<256, 16>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+        else if (lr > 0)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rowfft_update_tiled<256, 24>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
+        else
+            hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     }
-    if (lr > 0 && r16)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rowfft_update_tiled<256, 16>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
-    else if (lr > 0)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rowfft_update_tiled<256, 24>), rgrid, dim3(256), ldr, s, st, sa, pl, tw, lr);
-    else
-        hipLaunchKernelGGL(k_rowfft_update, dim3(st.nb, st.B), dim3(256), lds, s, st, sa, pl, tw);
     const int nrow = (sa.yc + st.r) / kTile - (sa.yc - st.r) / kTile + 1;
     const int ncol = (sa.xc + st.r) / kTile - (sa.xc - st.r) / kTile + 1;
     if (ncol > 8)

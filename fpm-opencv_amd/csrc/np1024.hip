@@ -1,0 +1,272 @@
+// np1024.hip -- the general path's row and column passes for Np = 1024
+// (BASELINE config 5: Np 1024, L 4096, naRadius 333, fp16 spectrum storage),
+// one 1024-point transform per wavefront held in registers (16 values per
+// lane) instead of mixed-radix Stockham passes over LDS tiles.
+//
+// Same three steps and the same scratch as general.hip's K1-K3
+// (fpmMain.cpp:358-447,457-464); K4/K5 (tile maxima, pupil commit) follow
+// unchanged:
+//   R1 k_rows1024_inv   a wave per support-box row: gather O*P on the disk,
+//                       row IDFT, T row stored as 128-byte segments
+//   C  k_cols1024       a block per 4 adjacent columns (a wave each): box rows
+//                       of T staged through an LDS strip, column IDFT,
+//                       amplitude replacement against the stack read
+//                       column-major (meas_layout g = Np), column DFT, box rows
+//                       back to T; blocks mapped so that one XCD owns a
+//                       contiguous run of columns (shared L2 lines of T)
+//   R2 k_rows1024_fwd   a wave per box row: T row in, row DFT, object update
+//                       and pupil numerator on the disk pixels of the row
+//
+// Config 5 holds only 8 patches, so one LED step is ~19 k transforms: too few
+// for a 16-lane group per transform to hide its serial latency (measured: a
+// 16-lane-group version at 1-2 waves per SIMD ran 45-88 us per launch).  A
+// wave per transform quarters the per-lane chain and needs far fewer VGPRs.
+//
+// Wave transform (lane = 16 c + t, group c < 4, t < 16), 1024 = 4 x 256:
+//   layout D (decimated): x[j]       = element 4 (t + 16 j) + c
+//   layout N (natural):   x[4 p + b] = element t + 16 (4 c + b) + 256 p
+//   D -> N (w1k_DN): group c runs the four-step 256-point DFT of sub-sequence
+//     c (dft256_full), a cross-group LDS exchange gives lane (c, t) the four
+//     sub-results at k' = t + 16 (4 c + b), then the radix-4 combine
+//     X[k' + 256 p] = sum_c' W1024^{c' k'} W4^{c' p} Y_c'[k'].
+//   N -> D (w1k_ND): the same steps transposed (radix-4 over p and the
+//     W1024^{c' k'} twiddles first, exchange, then the 256-point DFTs), since
+//     X[4 m + c] = sum_k' W256^{k' m} W1024^{k' c} sum_p x[k' + 256 p] W4^{p c}.
+#include <hip/hip_runtime.h>
+
+#include "dftL.hpp"
+#include "fpm_state.hpp"
+
+namespace fpm {
+
+namespace n1k {
+constexpr int N = 1024, H = N / 2;
+constexpr int WPB = 4;             // waves (rows / columns) per block
+constexpr int NT = 64 * WPB;
+constexpr int CXP = 17;            // cross-group exchange row pitch (complex)
+constexpr int WTILE = 4 * XTILE;   // per-wave LDS: four exchange16 tiles; the
+                                   // cross-group tile (4 x 16 x CXP) fits inside
+constexpr int SPC = WPB + 1;       // column-pass strip pitch (complex)
+static_assert(4 * 16 * CXP <= WTILE, "cross-group tile");
+}  // namespace n1k
+
+namespace {
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float2 w1024(const float2 *twL, int e, bool inv) {
+    const float2 w = twL[e & (n1k::N - 1)];
+    return inv ? cconj(w) : w;
+}
+
+// layout D -> layout N.  wt: this wave's LDS tile (n1k::WTILE complex)
+template <bool INV>
+__device__ __forceinline__ void w1k_DN(float2 (&x)[16], float2 *wt, const float2 *twL, int c, int t, int xrd) {
+    using namespace n1k;
+    float2 y[16];
+    dft256_full<INV>(x, y, wt + c * XTILE, LdsTw{twL, t, 4}, t, xrd);   // y[r] = Y_c[t + 16 r]
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wt[(c * 16 + r) * CXP + t] = y[r];
+    wave_sync();
+    const float2 *tl = fresh_lds(twL);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int kp = t + 16 * (4 * c + b);
+        float2 z[4];
+        z[0] = wt[(0 * 16 + 4 * c + b) * CXP + t];
+#pragma unroll
+        for (int cc = 1; cc < 4; ++cc) z[cc] = cmul(wt[(cc * 16 + 4 * c + b) * CXP + t], w1024(tl, cc * kp, INV));
+        dft4<INV>(z);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) x[4 * p + b] = z[p];
+    }
+    wave_sync();  // the tile is free for the next exchange
+}
+
+// layout N -> layout D
+template <bool INV>
+__device__ __forceinline__ void w1k_ND(float2 (&x)[16], float2 *wt, const float2 *twL, int c, int t, int xrd) {
+    using namespace n1k;
+    const float2 *tl = fresh_lds(twL);
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int kp = t + 16 * (4 * c + b);
+        float2 z[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) z[p] = x[4 * p + b];
+        dft4<INV>(z);
+        wt[(0 * 16 + 4 * c + b) * CXP + t] = z[0];
+#pragma unroll
+        for (int cc = 1; cc < 4; ++cc) wt[(cc * 16 + 4 * c + b) * CXP + t] = cmul(z[cc], w1024(tl, cc * kp, INV));
+    }
+    wave_sync();
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = wt[(c * 16 + r) * CXP + t];     // Z_c[t + 16 r]
+    wave_sync();
+    dft256_full<INV>(v, x, wt + c * XTILE, LdsTw{twL, t, 4}, t, xrd);   // x[j] = X[4 (t + 16 j) + c]
+}
+
+__device__ __forceinline__ int fold(int k) { return k < n1k::H ? k : k - n1k::N; }  // signed frequency
+
+// stage the N-point twiddle table; returns the table
+__device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__restrict__ tw) {
+    for (int i = threadIdx.x; i < n1k::N; i += n1k::NT) sm[i] = tw[i];
+    __syncthreads();
+    return sm;
+}
+
+// R1: grid (ceil(nb / WPB), B), block NT
+__global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+    using namespace n1k;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase(t);
+    const float2 *twL = stage_twiddles(sm, tw);
+    float2 *wt = sm + N + w * WTILE;
+    const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
+    if (row >= nb) return;  // wave-uniform; no block barrier follows
+    const int ky = row - r, w2 = r * r - ky * ky;
+    const float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;   // indexed by kx
+    const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;         // + kx (:358-362)
+    float2 x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int kx = fold(4 * (t + 16 * j) + c);
+        x[j] = kx * kx <= w2 ? cmul(spec_ld(st, b, srow + kx), pup[kx]) : make_float2(0.f, 0.f);  // :364
+    }
+    w1k_DN<true>(x, wt, twL, c, t, xrd);                                 // :365 (rows)
+    float2 *T = st.T + ((size_t)b * nb + row) * N + t + 64 * c;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) T[16 * bb + 256 * p] = x[4 * p + bb];
+}
+
+// C: grid (N / WPB, B), block NT
+__global__ void __launch_bounds__(n1k::NT) k_cols1024(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+    using namespace n1k;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase(t);
+    const float2 *twL = stage_twiddles(sm, tw);
+    float2 *strip = sm + N;            // N x SPC; the wave tiles alias it while
+    float2 *wt = strip + w * WTILE;    // every column is in registers
+    // XCD-aware column groups: the dispatcher deals blocks round-robin over the
+    // 8 XCDs, so XCD k gets column groups k*G/8 .. (k+1)*G/8 - 1 (contiguous)
+    constexpr int G = N / WPB;
+    const int cg = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);
+    const int r = st.r, nb = st.nb, b = blockIdx.y, x0 = cg * WPB;
+    float2 *T = st.T + (size_t)b * nb * N + x0;
+    // box row j holds FFT row i = j - r mod N (:364: every other row is zero)
+    for (int idx = threadIdx.x; idx < nb * WPB; idx += NT) {
+        const int j = idx / WPB, cc = idx - j * WPB, i = j - r < 0 ? j - r + N : j - r;
+        strip[i * SPC + cc] = T[(size_t)j * N + cc];
+    }
+    __syncthreads();
+    float2 x[16];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const int i = t + 16 * (4 * c + bb) + 256 * p;
+            x[4 * p + bb] = (i <= r || i >= N - r) ? strip[i * SPC + w] : make_float2(0.f, 0.f);
+        }
+    __syncthreads();
+    w1k_ND<true>(x, wt, twL, c, t, xrd);                                 // :365 (columns)
+    // amplitude replacement (:378-394) on row y = 4 (t + 16 j) + c of column
+    // x0 + w: with v the unscaled IDFT value, psi = v / N^2 and
+    // sqrt(I) psi / |psi + eps (1 + i)| = v / sqrt(|v + eps N^2 (1 + i)|^2 / I)
+    const float nn = (float)N * (float)N, epsn = st.eps * nn, epsn_im = st.eps_im * nn;
+    const uint16_t *Ic = st.meas + (((size_t)sa.led * st.B + b) * N + x0 + w) * N + c;  // meas_layout g = Np
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const float iv = (float)Ic[4 * (t + 16 * j)];
+        const float2 v = x[j];
+        const float tr = v.x + epsn, ti = v.y + epsn_im;
+        const float s = __builtin_amdgcn_rsqf(__builtin_fmaf(tr, tr, ti * ti) * __builtin_amdgcn_rcpf(iv));
+        x[j] = make_float2(v.x * s, v.y * s);
+    }
+    w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (columns)
+    __syncthreads();  // every wave is done with its tile before the strip is rewritten
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const int i = t + 16 * (4 * c + bb) + 256 * p;
+            if (i <= r || i >= N - r) strip[i * SPC + w] = x[4 * p + bb];
+        }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nb * WPB; idx += NT) {
+        const int j = idx / WPB, cc = idx - j * WPB, i = j - r < 0 ? j - r + N : j - r;
+        T[(size_t)j * N + cc] = strip[i * SPC + cc];
+    }
+}
+
+// R2: grid (ceil(nb / WPB), B), block NT
+__global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+    using namespace n1k;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    __shared__ float red[WPB];
+    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase(t);
+    const float2 *twL = stage_twiddles(sm, tw);
+    float2 *wt = sm + N + w * WTILE;
+    const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
+    // max|P| of the previous commit from its npart partial maxima (:415)
+    float pm = 0.f;
+    for (int i = threadIdx.x; i < st.npart; i += NT) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
+    pm = block_max(pm, red);
+    if (row >= nb) return;
+    const int ky = row - r, w2 = r * r - ky * ky;
+    const float2 *Tr = st.T + ((size_t)b * nb + row) * N + c;
+    float2 x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = Tr[4 * (t + 16 * j)];
+    w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (rows)
+    float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
+    float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
+    const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const int kx = fold(t + 16 * (4 * c + bb) + 256 * p);
+            if (kx * kx > w2) continue;
+            const size_t si = srow + kx;
+            const float2 o = spec_ld(st, b, si);                 // pre-update Objfcrop (:361)
+            const float2 pp = pup[kx];
+            const float2 D = csub(x[4 * p + bb], cmul(o, pp));   // Objfup - ObjfcropP (:409,463)
+            const float pa = cmag(pp);                           // object update (:406-419,433)
+            const float2 dpc = cmul(cmul(D, cscale(cconj(pp), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
+            spec_st(st, b, si, cadd(o, dpc));
+            const float oa = cmag(o);                            // pupil numerator (:459-464,469)
+            dP[kx] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
+        }
+}
+
+}  // namespace
+
+// Register path for this context?  Np 1024 with the stack in the transposed
+// layout (the caller permutes it when this returns true).
+bool np1024_supported(int np, int r) { return np == n1k::N && r >= 1 && r < n1k::H; }
+
+hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, hipStream_t s) {
+    using namespace n1k;
+    if (!np1024_supported(st.np, st.r) || st.meas_g != N) return hipErrorInvalidValue;
+    const size_t lds_r = (size_t)(N + WPB * WTILE) * sizeof(float2);
+    constexpr size_t strip = (size_t)N * SPC > (size_t)WPB * WTILE ? (size_t)N * SPC : (size_t)WPB * WTILE;
+    const size_t lds_c = (N + strip) * sizeof(float2);
+    hipError_t e = hipFuncSetAttribute((const void *)k_cols1024, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
+    if (e != hipSuccess) return e;
+    const dim3 rgrid((st.nb + WPB - 1) / WPB, st.B);
+    hipLaunchKernelGGL(k_rows1024_inv, rgrid, dim3(NT), lds_r, s, st, sa, tw);
+    hipLaunchKernelGGL(k_cols1024, dim3(N / WPB, st.B), dim3(NT), lds_c, s, st, sa, tw);
+    hipLaunchKernelGGL(k_rows1024_fwd, rgrid, dim3(NT), lds_r, s, st, sa, tw);
+    return hipGetLastError();
+}
+
+}  // namespace fpm

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dft16.hpp"
+#include "dftL.hpp"
 #include "dft200.hpp"
 #include "fpm_state.hpp"
 
@@ -36,63 +37,6 @@
 namespace fpm {
 
 namespace {
-
-// 256-point DFT of x[m] (m = t + 16 j held as v[j]) -> out[r] = X[t + 16 r]
-template <bool INV>
-__device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], float2 *scr,
-                                            const float2 (&wt)[16], int t, int xrd) {
-    float2 y[16];
-    dft16<INV>(v, y);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], INV ? cconj(wt[k1]) : wt[k1]);
-    float2 z[16];
-    exchange16(scr, t, xrd, y, z);
-    dft16<INV>(z, out);
-}
-
-template <int M, bool INV>
-__device__ __forceinline__ void dftM(float2 *v) {
-    if (M == 2) dft2<INV>(v);
-    if (M == 3) dft3<INV>(v);
-    if (M == 4) dft4<INV>(v);
-}
-
-// x[c][j] = element M*(t + 16 j) + c;  on return x[p][r] = X[t + 16 r + 256 p]
-template <int M, bool INV>
-__device__ __forceinline__ void dftL_regs(float2 (&x)[M][16], float2 *scr, const float2 (&wt)[16],
-                                          const float2 *twL, int t, int xrd) {
-#pragma unroll
-    for (int c = 0; c < M; ++c) {
-        float2 o[16];
-        dft256_full<INV>(x[c], o, scr, wt, t, xrd);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) x[c][r] = o[r];
-    }
-    constexpr int L = 256 * M;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int kp = t + 16 * r;
-        float2 z[M];
-        z[0] = x[0][r];
-#pragma unroll
-        for (int c = 1; c < M; ++c) {
-            const float2 w = twL[(c * kp) % L];
-            z[c] = cmul(x[c][r], INV ? cconj(w) : w);
-        }
-        dftM<M, INV>(z);
-#pragma unroll
-        for (int p = 0; p < M; ++p) x[p][r] = z[p];
-    }
-}
-
-// per-lane four-step twiddles W256^{m t} and the W_L table, staged in LDS
-__device__ __forceinline__ void load_twiddles(float2 *twL, const float2 *__restrict__ tw_L, int L, int step,
-                                              float2 (&wt)[16], int t) {
-    for (int i = threadIdx.x; i < L; i += blockDim.x) twL[i] = tw_L[i];
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 16; ++m) wt[m] = twL[((m * t) & 255) * step];  // W256^{mt} = W_L^{M m t}
-}
 
 // live-band test: a <= i <= b
 __device__ __forceinline__ bool in_band(int i, int a, int b) { return (unsigned)(i - a) <= (unsigned)(b - a); }

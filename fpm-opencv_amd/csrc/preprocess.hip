@@ -147,9 +147,36 @@ __global__ void __launch_bounds__(1024) k_meas_transpose(uint16_t *meas, int np,
         p[i] = tl[b * ld + a];
     }
 }
+// g = Np for large Np (the Np 1024 register kernels, np1024.hip): in-place
+// transpose by 64 x 64 tile pairs (ti, tj), ti <= tj, swapped through LDS.
+// grid (nt (nt + 1) / 2, nimg), block 256
+__global__ void __launch_bounds__(256) k_meas_transpose_tiles(uint16_t *meas, int np, size_t nimg) {
+    __shared__ uint16_t ta[64][66], tb[64][66];
+    const int nt = np / 64;
+    int q = blockIdx.x, ti = 0;
+    while (q >= nt - ti) {
+        q -= nt - ti;
+        ++ti;
+    }
+    const int tj = ti + q;
+    uint16_t *p = meas + (size_t)blockIdx.y * np * np;
+    uint16_t *a = p + (size_t)ti * 64 * np + tj * 64, *bb = p + (size_t)tj * 64 * np + ti * 64;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int y = i >> 6, x = i & 63;
+        ta[y][x] = a[(size_t)y * np + x];
+        tb[y][x] = bb[(size_t)y * np + x];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int y = i >> 6, x = i & 63;
+        bb[(size_t)y * np + x] = ta[x][y];
+        a[(size_t)y * np + x] = tb[x][y];
+    }
+}
 }  // namespace
 
-// g = 16 (Np 256 fused kernel), 10 (Np 200 fused kernel) or Np (small-patch kernel)
+// g = 16 (Np 256 fused kernel), 10 (Np 200 fused kernel) or Np (small-patch
+// kernel, Np 1024 register kernels: the plain transpose)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s) {
     if (np == 256 && g == 16) return launch_layout<256, 16>(meas, nimg, fwd, s);
     if (np == 200 && g == 10) return launch_layout<200, 10>(meas, nimg, fwd, s);
@@ -157,6 +184,13 @@ hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hip
         if (nimg == 0) return hipSuccess;
         const size_t lds = (size_t)np * (np + 2) * sizeof(uint16_t);
         hipLaunchKernelGGL(k_meas_transpose, dim3((unsigned)nimg), dim3(1024), lds, s, meas, np, nimg);
+        return hipGetLastError();
+    }
+    if (g == np && np % 64 == 0) {
+        if (nimg == 0) return hipSuccess;
+        const int nt = np / 64;
+        hipLaunchKernelGGL(k_meas_transpose_tiles, dim3(nt * (nt + 1) / 2, (unsigned)nimg), dim3(256), 0, s, meas,
+                           np, nimg);
         return hipGetLastError();
     }
     return hipErrorInvalidValue;
