@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,7 +41,7 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
 bool fused_small_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                         const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                        const FftPlan &pl, hipStream_t s);
+                                        const FftPlan &pl, unsigned long long *dbg, hipStream_t s);
 // Np 1024 register row/column kernels of the general path (np1024.hip)
 bool np1024_supported(int np, int r);
 size_t fused_park_elems(int nt, int B);
@@ -550,7 +551,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
         if (c->path == FPM_PATH_FUSED && c->fused_small) {
             HIP_TRY(launch_fused_small_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
-                                                 c->prob.n_order, c->tw_np, c->pl_np, c->stream));
+                                                 c->prob.n_order, c->tw_np, c->pl_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED && c->fused_mr) {
             HIP_TRY(launch_fused_mr_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));

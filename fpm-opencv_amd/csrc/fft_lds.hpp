@@ -116,6 +116,79 @@ __device__ __forceinline__ void dft5(float2 *v) {
     v[3] = csub(r2, iq2);
 }
 
+// ---- composite radices R = A*B (A, B in {2, 3, 4, 5}) in registers --------
+// One Stockham pass of radix 6/9/10/12/15 replaces two passes of its factors
+// (half the LDS round trips and barriers of the small-patch kernel, whose
+// Np = 90 = 2*3*3*5 otherwise takes four passes per transform: stockham_t).
+// X[k1 + A k2] = sum_n2 W_B^{n2 k2} W_R^{n2 k1} sum_n1 v[B n1 + n2] W_A^{n1 k1}
+// with compile-time twiddles W_R^m.
+namespace cwt {
+constexpr double kPi = 3.14159265358979323846;
+// cos / sin by Taylor series of |x| <= pi after reduction (compile time only)
+constexpr double csin(double x) {
+    double t = x, s = x;
+    for (int i = 1; i < 20; ++i) {
+        t *= -x * x / ((2 * i) * (2 * i + 1));
+        s += t;
+    }
+    return s;
+}
+constexpr double ccos(double x) {
+    double t = 1, s = 1;
+    for (int i = 1; i < 20; ++i) {
+        t *= -x * x / ((2 * i - 1) * (2 * i));
+        s += t;
+    }
+    return s;
+}
+// W_R^m = exp(-2 pi i m / R) as (cos, sin) of the reduced angle
+constexpr double wang(int R, int m) {
+    const int q = ((m % R) + R) % R;
+    const double a = -2.0 * kPi * q / R;
+    return a < -kPi ? a + 2.0 * kPi : a;
+}
+}  // namespace cwt
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft_prime(float2 *v) {
+    if constexpr (R == 2) dft2<INV>(v);
+    if constexpr (R == 3) dft3<INV>(v);
+    if constexpr (R == 4) dft4<INV>(v);
+    if constexpr (R == 5) dft5<INV>(v);
+}
+
+template <int A, int B, bool INV>
+__device__ __forceinline__ void dft_ab(float2 *v) {
+    constexpr int R = A * B;
+    float2 y[R];
+#pragma unroll
+    for (int n2 = 0; n2 < B; ++n2) {
+        float2 t[A];
+#pragma unroll
+        for (int n1 = 0; n1 < A; ++n1) t[n1] = v[B * n1 + n2];
+        dft_prime<A, INV>(t);
+#pragma unroll
+        for (int k1 = 0; k1 < A; ++k1) {
+            if ((n2 * k1) % R == 0) {
+                y[k1 * B + n2] = t[k1];
+            } else {
+                const float c = (float)cwt::ccos(cwt::wang(R, n2 * k1));
+                const float sn = (float)cwt::csin(cwt::wang(R, n2 * k1)) * (INV ? -1.f : 1.f);
+                y[k1 * B + n2] = cmul(t[k1], make_float2(c, sn));
+            }
+        }
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < A; ++k1) {
+        float2 u[B];
+#pragma unroll
+        for (int n2 = 0; n2 < B; ++n2) u[n2] = y[k1 * B + n2];
+        dft_prime<B, INV>(u);
+#pragma unroll
+        for (int k2 = 0; k2 < B; ++k2) v[k1 + A * k2] = u[k2];
+    }
+}
+
 // a / d for 0 <= a < 2^22 via the float reciprocal rd = 1/d and one
 // correction step (an integer division by a runtime value costs ~40 VALU
 // instructions on CDNA; this is 6)
@@ -159,6 +232,11 @@ __device__ __forceinline__ void stockham_pass(const float2 *__restrict__ a, floa
         if (R == 4) dft4<INV>(v);
         if (R == 5) dft5<INV>(v);
         if (R == 8) dft8<INV>(v);
+        if constexpr (R == 6) dft_ab<2, 3, INV>(v);
+        if constexpr (R == 9) dft_ab<3, 3, INV>(v);
+        if constexpr (R == 10) dft_ab<2, 5, INV>(v);
+        if constexpr (R == 12) dft_ab<4, 3, INV>(v);
+        if constexpr (R == 15) dft_ab<3, 5, INV>(v);
         const int base = jq * Ns * R + k;
 #pragma unroll
         for (int r = 0; r < R; ++r) dst[base + r * Ns] = v[r];
@@ -188,6 +266,21 @@ __device__ float2 *stockham(float2 *a, float2 *b, int C, const FftPlan &pl,
         Ns *= R;
     }
     return a;
+}
+
+// stockham() with the transform length N and the radices fixed at compile
+// time (the small-patch kernel's Np 90 = 10 x 9 instance): no radix switch,
+// constant strides and divisors.  Ends with a barrier; returns the result buffer.
+template <bool INV, int N, int NS, int R, int... REST>
+__device__ __forceinline__ float2 *stockham_t(float2 *a, float2 *b, int C, const float2 *__restrict__ tw, int tid,
+                                              int nthr) {
+    stockham_pass<R, INV>(a, b, N, C, NS, tw, tid, nthr);
+    __syncthreads();
+    if constexpr (sizeof...(REST) == 0) {
+        return b;
+    } else {
+        return stockham_t<INV, N, NS * R, REST...>(b, a, C, tw, tid, nthr);
+    }
 }
 
 // ---- block reductions -------------------------------------------------------

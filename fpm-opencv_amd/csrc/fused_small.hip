@@ -31,6 +31,10 @@
 
 namespace fpm {
 
+#ifndef FPM_SMALL_STAMPS
+#define FPM_SMALL_STAMPS 0  // 1: phase stamps (FPM_STAMPS=1); compiled out by default (register pressure)
+#endif
+
 namespace fs {
 constexpr int NT = 1024;
 constexpr int SP = 4;        // support-box pixels per thread: nb^2 <= NT * SP (r <= 31)
@@ -42,19 +46,30 @@ struct SmallArgs {
     const uint16_t *meas;   // [nS][B][x][y] = I[y][x] (meas_layout with g = Np)
     const int *order, *x0, *y0;
     const float2 *tw;       // exp(-2 pi i k / Np), k < Np
-    FftPlan pl;             // mixed-radix plan of Np
+    FftPlan pl;             // mixed-radix plan of Np (the generic instance)
     int n_order;
     int btx0, bty0, nbx, nbt;  // live-band tiles (fpm_fused.hip FusedArgs)
     float rnbx;
+    unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles, else null
 };
 
+// NPC = 90: Np and the plan fixed at compile time, two composite-radix passes
+// 10 x 9 per transform (BASELINE configs 1/2; the runtime plan 2*3*3*5 takes
+// four passes and, with a radix switch at each of the four call sites, more
+// registers: 1.89 M -> 3.19 M LED-updates/s at config 2); NPC = 0: any
+// Np <= 96 with the runtime plan
+template <int NPC>
 __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
     using namespace fs;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const DevState &st = a.st;
-    const int Np = st.np, L = st.L, R = st.r, NB = st.nb, NN = Np * Np;
+    const int Np = NPC ? NPC : st.np, L = st.L, R = st.r, NB = st.nb, NN = Np * Np;
+
     float2 *A = sm, *Bf = sm + NN, *twl = Bf + NN;
     float *tmx = (float *)(twl + Np);                  // band-tile maxima
+#define FPM_SMALL_FFT(INV, x, y, C)                                                        \
+    (NPC == 90 ? stockham_t<INV, 90, 1, 10, 9>((x), (y), (C), twl, tid, NT) \
+               : stockham<INV>((x), (y), (C), a.pl, twl, tid, NT))
     unsigned *dirty = (unsigned *)(tmx + a.nbt);       // band-tile dirty bits
     float *red = (float *)(dirty + ((a.nbt + 31) >> 5));  // 3 x 16: per-wave maxima
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x;
@@ -117,6 +132,14 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
     };
     auto fidx = [&](int k) { return k < 0 ? k + Np : k; };  // FFT index of frequency k, |k| < Np
 
+    unsigned long long acc[kStamps] = {};
+    unsigned long long prev = (FPM_SMALL_STAMPS && a.dbg) ? __builtin_amdgcn_s_memtime() : 0ull;
+#define FPM_STAMP(i)                                                  \
+    if (FPM_SMALL_STAMPS && a.dbg) {                                  \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        acc[i] += now_ - prev;                                        \
+        prev = now_;                                                  \
+    }
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
         const int xc = a.x0[led] + Np / 2, yc = a.y0[led] + Np / 2;
@@ -134,8 +157,10 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                 A[(ky + R) * Np + fidx(kx)] = pout(pmul(pin(Op[i]), pin(P[i])));
             }
         __syncthreads();
+        FPM_STAMP(0)
         // ---- row IDFTs of the box rows, then column-major with zero rows (:365)
-        float2 *res = stockham<true>(A, Bf, NB, a.pl, twl, tid, NT);
+        float2 *res = FPM_SMALL_FFT(true, A, Bf, NB);
+        FPM_STAMP(7)
         float2 *col = res == A ? Bf : A;
         for (int e = tid; e < NN; e += NT) {
             const int x = e / Np, y = e - x * Np;
@@ -143,7 +168,9 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             col[e] = (ky >= -R && ky <= R) ? res[(ky + R) * Np + x] : make_float2(0.f, 0.f);
         }
         __syncthreads();
-        col = stockham<true>(col, res, Np, a.pl, twl, tid, NT);
+        FPM_STAMP(1)
+        col = FPM_SMALL_FFT(true, col, res, Np);
+        FPM_STAMP(10)
         // ---- amplitude replacement (:365-394): psi = r/Np^2,
         // sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I), eps on both channels (:390)
         for (int e = tid; e < NN; e += NT) {
@@ -154,7 +181,9 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             col[e] = pout(r * __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(Iv)));
         }
         __syncthreads();
-        float2 *colF = stockham<false>(col, col == A ? Bf : A, Np, a.pl, twl, tid, NT);
+        FPM_STAMP(2)
+        float2 *colF = FPM_SMALL_FFT(false, col, col == A ? Bf : A, Np);
+        FPM_STAMP(8)
         // ---- back to the box rows, row DFTs (:394)
         float2 *rw = colF == A ? Bf : A;
         for (int e = tid; e < NB * Np; e += NT) {
@@ -162,7 +191,9 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             rw[e] = colF[x * Np + fidx(row - R)];
         }
         __syncthreads();
-        const float2 *F = stockham<false>(rw, colF, NB, a.pl, twl, tid, NT);
+        FPM_STAMP(3)
+        const float2 *F = FPM_SMALL_FFT(false, rw, colF, NB);
+        FPM_STAMP(9)
 
         // ---- object update on the support (:405-447), pupil numerator (:457-464)
 #pragma unroll
@@ -178,6 +209,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             }
         __syncthreads();  // spectrum writes, tile maxima, dirty bits
         if (it + 1 < a.n_order) loadO(window(it + 1));
+        FPM_STAMP(4)
 
         // ---- exact max|objF| (:460,467) from the band-tile maxima
         float cm = 0.f, dm = 0.f;
@@ -230,6 +262,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
 #pragma unroll
             for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
         }
+        FPM_STAMP(5)
         const float rom = 1.0f / omax;
         // ---- P += num / max|objF| on the support (:468-475); max|P| (:415)
         float pmx = 0.f;
@@ -245,7 +278,12 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
 #pragma unroll
         for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
         pm = sqrtf(pm2);
+        FPM_STAMP(6)
     }
+#undef FPM_STAMP
+#undef FPM_SMALL_FFT
+    if (FPM_SMALL_STAMPS && a.dbg && (tid == 0 || tid == NT - 64))
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
 
 #pragma unroll
     for (int i = 0; i < SP; ++i)
@@ -285,7 +323,7 @@ bool fused_small_supported(int np, int r, const DevState &st) {
 
 hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                         const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                        const FftPlan &pl, hipStream_t s) {
+                                        const FftPlan &pl, unsigned long long *dbg, hipStream_t s) {
     if (!fused_small_supported(st.np, st.r, st)) return hipErrorInvalidValue;
     SmallArgs a;
     a.st = st;
@@ -295,6 +333,7 @@ hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas
     a.y0 = y0_dev;
     a.tw = tw_np;
     a.pl = pl;
+    a.dbg = dbg;
     a.n_order = n_order;
     const SmallBand bd = small_band(st);
     a.bty0 = bd.bty0;
@@ -303,10 +342,15 @@ hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas
     a.nbt = bd.nbt;
     a.rnbx = 1.0f / (float)a.nbx;
     const size_t lds = small_lds_bytes(st.np, a.nbt);
-    hipError_t e =
-        hipFuncSetAttribute((const void *)k_fused_small, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // Np 90 (configs 1/2): the instance with the transform fixed at compile time
+    const bool c90 = st.np == 90;
+    const void *fn = c90 ? (const void *)k_fused_small<90> : (const void *)k_fused_small<0>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_fused_small, dim3(st.B), dim3(fs::NT), lds, s, a);
+    if (c90)
+        hipLaunchKernelGGL(k_fused_small<90>, dim3(st.B), dim3(fs::NT), lds, s, a);
+    else
+        hipLaunchKernelGGL(k_fused_small<0>, dim3(st.B), dim3(fs::NT), lds, s, a);
     return hipGetLastError();
 }
 
