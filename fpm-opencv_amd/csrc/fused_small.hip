@@ -39,6 +39,7 @@ namespace fs {
 constexpr int NT = 1024;
 constexpr int SP = 4;        // support-box pixels per thread: nb^2 <= NT * SP (r <= 31)
 constexpr int NPMAX = 96;    // two Np x Np complex buffers in 160 KB of LDS
+constexpr int KM = (90 * 90 / 2 + NT - 1) / NT;  // Np 90: measurement dwords per thread
 }  // namespace fs
 
 struct SmallArgs {
@@ -72,6 +73,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                : stockham<INV>((x), (y), (C), a.pl, twl, tid, NT))
     unsigned *dirty = (unsigned *)(tmx + a.nbt);       // band-tile dirty bits
     float *red = (float *)(dirty + ((a.nbt + 31) >> 5));  // 3 x 16: per-wave maxima
+    uint16_t *ims = (uint16_t *)(red + 48);               // Np 90: staged measurement image
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x;
     constexpr int NW = NT / 64;
     const int nwords = (a.nbt + 31) >> 5;
@@ -145,6 +147,19 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
         const int xc = a.x0[led] + Np / 2, yc = a.y0[led] + Np / 2;
         float2 *srow = spec + (unsigned)(yc * L + xc);  // spec[yc + ky][xc + kx] = srow[ky*L + kx]
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NN;
+        // Np 90: the image is staged in LDS (ims) -- loaded here, stored after
+        // the gather -- so the amplitude step does not wait on HBM latency
+        // (amplitude 7.1k -> 2.2k cycles per LED; storing it after the row
+        // IDFTs instead measured no better)
+        uint32_t mreg[KM];
+        if constexpr (NPC == 90) {
+            const uint32_t *I32 = (const uint32_t *)Ib;  // NN even: 4-byte aligned images
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+                const int i = tid + NT * k;
+                mreg[k] = i < NN / 2 ? I32[i] : 0u;
+            }
+        }
 
         // ---- gather O*P into the box rows (:358-364)
         for (int e = tid; e < NB * Np; e += NT) A[e] = make_float2(0.f, 0.f);
@@ -156,6 +171,14 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                 pix(i, ky, kx);
                 A[(ky + R) * Np + fidx(kx)] = pout(pmul(pin(Op[i]), pin(P[i])));
             }
+        if constexpr (NPC == 90) {  // read after the row/column IDFT barriers
+            uint32_t *ims32 = (uint32_t *)ims;
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+                const int i = tid + NT * k;
+                if (i < NN / 2) ims32[i] = mreg[k];
+            }
+        }
         __syncthreads();
         FPM_STAMP(0)
         // ---- row IDFTs of the box rows, then column-major with zero rows (:365)
@@ -174,7 +197,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
         // ---- amplitude replacement (:365-394): psi = r/Np^2,
         // sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I), eps on both channels (:390)
         for (int e = tid; e < NN; e += NT) {
-            const float Iv = (float)Ib[e];
+            const float Iv = (float)(NPC == 90 ? ims[e] : Ib[e]);
             const pf2 r = pin(col[e]);
             const pf2 tt = r + (pf2){epsn, epsn_im};
             const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
@@ -308,7 +331,8 @@ SmallBand small_band(const DevState &st) {
 }
 size_t small_lds_bytes(int np, int nbt) {
     return (size_t)(2 * np * np + np) * sizeof(float2) + (size_t)nbt * sizeof(float) +
-           (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 48 * sizeof(float);
+           (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 48 * sizeof(float) +
+           (np == 90 ? (size_t)np * np * sizeof(uint16_t) : 0);  // the Np 90 instance's staged image
 }
 }  // namespace
 

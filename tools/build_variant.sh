@@ -10,7 +10,7 @@ OUT=lib_var/$NAME
 mkdir -p $OUT/obj
 F="--offload-arch=gfx950 -O3 -fno-slp-vectorize -std=c++17 -fPIC -Wall -Wno-unused-result -I../include $EXTRA"
 pids=()
-for s in general fpm_fused fused_mr objcrop preprocess; do
+for s in $(cd csrc && ls *.hip | sed "s/\.hip$//"); do
   /opt/rocm/bin/hipcc $F -c csrc/$s.hip -o $OUT/obj/$s.o & pids+=($!)
 done
 /opt/rocm/bin/hipcc $F -x hip -c csrc/api.cpp -o $OUT/obj/api.o & pids+=($!)
