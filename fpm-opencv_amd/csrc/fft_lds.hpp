@@ -283,6 +283,43 @@ __device__ __forceinline__ float2 *stockham_t(float2 *a, float2 *b, int C, const
     }
 }
 
+// any supported radix in registers
+template <int R, bool INV>
+__device__ __forceinline__ void dft_any(float2 *v) {
+    if constexpr (R == 2 || R == 3 || R == 4 || R == 5) dft_prime<R, INV>(v);
+    if constexpr (R == 8) dft8<INV>(v);
+    if constexpr (R == 6) dft_ab<2, 3, INV>(v);
+    if constexpr (R == 9) dft_ab<3, 3, INV>(v);
+    if constexpr (R == 10) dft_ab<2, 5, INV>(v);
+    if constexpr (R == 12) dft_ab<4, 3, INV>(v);
+    if constexpr (R == 15) dft_ab<3, 5, INV>(v);
+}
+
+// stockham_t whose first pass (Ns = 1: no twiddles) takes its inputs from a
+// loader ld(s, i) = element i of sequence s instead of an LDS buffer, so a
+// gather or a transpose folds into the transform; the first pass writes `a`.
+template <bool INV, int N, int R, int... REST, class LD>
+__device__ __forceinline__ float2 *stockham_t_ld(const LD &ld, float2 *a, float2 *b, int C,
+                                                 const float2 *__restrict__ tw, int tid, int nthr) {
+    constexpr int NR = N / R;
+    for (int jj = tid; jj < C * NR; jj += nthr) {
+        const int s = jj / NR, j = jj - s * NR;
+        float2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = ld(s, j + r * NR);
+        dft_any<R, INV>(v);
+        float2 *dst = a + s * N + j * R;
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[r] = v[r];
+    }
+    __syncthreads();
+    if constexpr (sizeof...(REST) == 0) {
+        return a;
+    } else {
+        return stockham_t<INV, N, R, REST...>(a, b, C, tw, tid, nthr);
+    }
+}
+
 // ---- block reductions -------------------------------------------------------
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

@@ -161,6 +161,63 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             }
         }
 
+        const float2 *F;
+        if constexpr (NPC == 90) {
+            // Gather and both transposes folded into the transforms' first
+            // passes (stockham_t_ld): the owners write the support box densely
+            // (O*P on the disk, 0 elsewhere) into Bf, the row IDFT's first pass
+            // reads it as box rows, the column passes read the other
+            // orientation in place -- no zero fill and no transpose passes.
+#pragma unroll
+            for (int i = 0; i < SP; ++i) {
+                const int p = tid + NT * i;
+                if (p < NB * NB)
+                    Bf[p] = ((inm >> i) & 1) ? pout(pmul(pin(Op[i]), pin(P[i]))) : make_float2(0.f, 0.f);  // :358-364
+            }
+            {  // read after the row/column IDFT barriers
+                uint32_t *ims32 = (uint32_t *)ims;
+#pragma unroll
+                for (int k = 0; k < KM; ++k) {
+                    const int i = tid + NT * k;
+                    if (i < NN / 2) ims32[i] = mreg[k];
+                }
+            }
+            __syncthreads();
+            FPM_STAMP(0)
+            // row IDFTs (:365): element i of box row s is frequency kx = i (i <= R) or i - Np
+            const float2 *box = Bf;
+            float2 *res = stockham_t_ld<true, 90, 10, 9>(
+                [&](int s, int i) {
+                    const int kx = i <= R ? i : i - Np;
+                    return (kx >= -R && kx <= R) ? box[s * NB + kx + R] : make_float2(0.f, 0.f);
+                },
+                A, Bf, NB, twl, tid, NT);  // -> Bf
+            FPM_STAMP(7)
+            // column IDFTs: element y of column x is box row ky = y (y <= R) or y - Np of res
+            float2 *col = stockham_t_ld<true, 90, 10, 9>(
+                [&](int x, int y) {
+                    const int ky = y <= R ? y : y - Np;
+                    return (ky >= -R && ky <= R) ? res[(ky + R) * Np + x] : make_float2(0.f, 0.f);
+                },
+                A, Bf, Np, twl, tid, NT);  // -> Bf
+            FPM_STAMP(10)
+            // ---- amplitude replacement (:365-394), see the generic branch
+            for (int e = tid; e < NN; e += NT) {
+                const float Iv = (float)ims[e];
+                const pf2 r = pin(col[e]);
+                const pf2 tt = r + (pf2){epsn, epsn_im};
+                const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
+                col[e] = pout(r * __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(Iv)));
+            }
+            __syncthreads();
+            FPM_STAMP(2)
+            float2 *colF = stockham_t<false, 90, 1, 10, 9>(col, A, Np, twl, tid, NT);  // -> Bf
+            FPM_STAMP(8)
+            // row DFTs (:394): element x of box row s is column x's FFT row fidx(s - R)
+            F = stockham_t_ld<false, 90, 10, 9>(
+                [&](int s, int x) { return colF[x * Np + fidx(s - R)]; }, A, Bf, NB, twl, tid, NT);  // -> Bf
+            FPM_STAMP(9)
+        } else {
         // ---- gather O*P into the box rows (:358-364)
         for (int e = tid; e < NB * Np; e += NT) A[e] = make_float2(0.f, 0.f);
         __syncthreads();
@@ -171,14 +228,6 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                 pix(i, ky, kx);
                 A[(ky + R) * Np + fidx(kx)] = pout(pmul(pin(Op[i]), pin(P[i])));
             }
-        if constexpr (NPC == 90) {  // read after the row/column IDFT barriers
-            uint32_t *ims32 = (uint32_t *)ims;
-#pragma unroll
-            for (int k = 0; k < KM; ++k) {
-                const int i = tid + NT * k;
-                if (i < NN / 2) ims32[i] = mreg[k];
-            }
-        }
         __syncthreads();
         FPM_STAMP(0)
         // ---- row IDFTs of the box rows, then column-major with zero rows (:365)
@@ -197,7 +246,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
         // ---- amplitude replacement (:365-394): psi = r/Np^2,
         // sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I), eps on both channels (:390)
         for (int e = tid; e < NN; e += NT) {
-            const float Iv = (float)(NPC == 90 ? ims[e] : Ib[e]);
+            const float Iv = (float)Ib[e];
             const pf2 r = pin(col[e]);
             const pf2 tt = r + (pf2){epsn, epsn_im};
             const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
@@ -215,8 +264,9 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
         }
         __syncthreads();
         FPM_STAMP(3)
-        const float2 *F = FPM_SMALL_FFT(false, rw, colF, NB);
+        F = FPM_SMALL_FFT(false, rw, colF, NB);
         FPM_STAMP(9)
+        }
 
         // ---- object update on the support (:405-447), pupil numerator (:457-464)
 #pragma unroll
