@@ -142,24 +142,24 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
         acc[i] += now_ - prev;                                        \
         prev = now_;                                                  \
     }
+    // Np 90: each LED's image is staged in LDS (ims) -- loaded into mreg one
+    // LED ahead (with the next window's O), stored with the gather -- so the
+    // amplitude step does not wait on HBM latency (7.1k -> 2.2k cycles per LED)
+    uint32_t mreg[KM];
+    auto load_meas = [&](int itn) {
+        const uint32_t *I32 = (const uint32_t *)(a.meas + ((size_t)a.order[itn] * st.B + b) * NN);  // NN even
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+            const int i = tid + NT * k;
+            mreg[k] = i < NN / 2 ? I32[i] : 0u;
+        }
+    };
+    if (NPC == 90 && a.n_order > 0) load_meas(0);
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
         const int xc = a.x0[led] + Np / 2, yc = a.y0[led] + Np / 2;
         float2 *srow = spec + (unsigned)(yc * L + xc);  // spec[yc + ky][xc + kx] = srow[ky*L + kx]
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NN;
-        // Np 90: the image is staged in LDS (ims) -- loaded here, stored after
-        // the gather -- so the amplitude step does not wait on HBM latency
-        // (amplitude 7.1k -> 2.2k cycles per LED; storing it after the row
-        // IDFTs instead measured no better)
-        uint32_t mreg[KM];
-        if constexpr (NPC == 90) {
-            const uint32_t *I32 = (const uint32_t *)Ib;  // NN even: 4-byte aligned images
-#pragma unroll
-            for (int k = 0; k < KM; ++k) {
-                const int i = tid + NT * k;
-                mreg[k] = i < NN / 2 ? I32[i] : 0u;
-            }
-        }
 
         const float2 *F;
         if constexpr (NPC == 90) {
@@ -281,7 +281,10 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                 note(yc + ky, xc + kx, oa, cmag(nv));
             }
         __syncthreads();  // spectrum writes, tile maxima, dirty bits
-        if (it + 1 < a.n_order) loadO(window(it + 1));
+        if (it + 1 < a.n_order) {
+            loadO(window(it + 1));
+            if (NPC == 90) load_meas(it + 1);
+        }
         FPM_STAMP(4)
 
         // ---- exact max|objF| (:460,467) from the band-tile maxima
