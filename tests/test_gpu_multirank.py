@@ -6,7 +6,8 @@ bit for bit (patches are independent; shards change nothing inside a patch).
 
 Inputs are seeded per GLOBAL patch index (tools/synth.make_stack seeds patch
 b with seed + b), so a shard's data does not depend on the shard layout.
-Both the fused (Np 256) and the general (Np 64) paths are covered.
+The fused (Np 256), the small-patch fused (Np 64) and the general (Np 64,
+forced) paths are covered.
 """
 import os
 import socket
@@ -20,7 +21,8 @@ GRID = (2, 3)
 TOTAL = GRID[0] * GRID[1]
 CASES = {
     "fused": dict(Np=256, L=512, r=20, n_side=3, step=24, d1=10, d2=3, iters=1),
-    "general": dict(Np=64, L=192, r=10, n_side=5, step=6, d1=5, d2=10, iters=2),
+    "general": dict(Np=64, L=192, r=10, n_side=5, step=6, d1=5, d2=10, iters=2, general=True),
+    "small": dict(Np=64, L=192, r=10, n_side=5, step=6, d1=5, d2=10, iters=2),  # small-patch fused kernel
 }
 SEED = 7100
 
@@ -29,7 +31,9 @@ def _problem(c, n_patch):
     import fpm_amd
     from tools.synth import grid_geometry
     x0, y0, order = grid_geometry(c["Np"], c["L"], c["n_side"], c["step"])
-    return fpm_amd.Problem(c["Np"], c["L"], order, x0, y0, c["r"], c["d1"], c["d2"], n_patch=n_patch), x0, y0
+    path = fpm_amd.PATH_GENERAL if c.get("general") else fpm_amd.PATH_AUTO
+    return fpm_amd.Problem(c["Np"], c["L"], order, x0, y0, c["r"], c["d1"], c["d2"], n_patch=n_patch,
+                           path=path), x0, y0
 
 
 def _solve(c, lo, hi):
@@ -73,7 +77,7 @@ def _rank_main(rank, world, port, name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["fused", "general"])
+@pytest.mark.parametrize("name", ["fused", "general", "small"])
 def test_two_ranks_stitched_field_equals_single_rank(name):
     import torch.multiprocessing as mp
     import fpm_amd
@@ -88,7 +92,7 @@ def test_two_ranks_stitched_field_equals_single_rank(name):
     for p in procs:
         p.join(180)
         assert p.exitcode == 0
-    want_path = fpm_amd.PATH_FUSED if name == "fused" else fpm_amd.PATH_GENERAL
+    want_path = fpm_amd.PATH_GENERAL if name == "general" else fpm_amd.PATH_FUSED
     assert path == want_path
     tiles, path1 = _solve(CASES[name], 0, TOTAL)
     assert path1 == want_path
