@@ -132,4 +132,29 @@ __device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const fl
     }
 }
 
+// Half-tile exchange: the same result through an 8-row tile (8 x XP complex,
+// half of XTILE) in two rounds -- rows y[0..7] written, lanes t < 8 read
+// theirs; rows y[8..15] written over them, lanes t >= 8 read.  The second
+// round's writes stay behind the first round's reads because the read base
+// (exch_rbase_half) is laundered like exch_rbase's.
+constexpr int XTILE_H = 8 * XP;
+__device__ __forceinline__ int exch_rbase_half(int t) { return opaque_int((t & 7) * XP); }
+__device__ __forceinline__ void exchange16_half(float2 *scr, int t, int xrdh, const float2 (&y)[16],
+                                                float2 (&z)[16]) {
+    const float4 *rp = (const float4 *)(scr + xrdh);  // 16-B aligned: XP even
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[8 * h + m1];
+        if ((t >> 3) == h) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 q = rp[j];
+                z[2 * j] = make_float2(q.x, q.y);
+                z[2 * j + 1] = make_float2(q.z, q.w);
+            }
+        }
+    }
+}
+
 }  // namespace fpm

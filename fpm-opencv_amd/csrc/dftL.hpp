@@ -28,7 +28,8 @@ __device__ __forceinline__ const float2 (&fresh_tw(const float2 (&w)[16]))[16] {
 __device__ __forceinline__ LdsTw fresh_tw(const LdsTw &w) { return LdsTw{fresh_lds(w.twL), w.t, w.step}; }
 
 // 256-point DFT of x[m] (m = t + 16 j held as v[j]) -> out[r] = X[t + 16 r]
-template <bool INV, typename TW>
+// HX: half-tile exchange (scr holds XTILE_H complex, xrd = exch_rbase_half(t))
+template <bool INV, bool HX = false, typename TW>
 __device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], float2 *scr,
                                             const TW &wt, int t, int xrd) {
     float2 y[16];
@@ -37,7 +38,10 @@ __device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], 
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) y[k1] = cmul(y[k1], INV ? cconj(w[k1]) : w[k1]);
     float2 z[16];
-    exchange16(scr, t, xrd, y, z);
+    if constexpr (HX)
+        exchange16_half(scr, t, xrd, y, z);
+    else
+        exchange16(scr, t, xrd, y, z);
     dft16<INV>(z, out);
 }
 

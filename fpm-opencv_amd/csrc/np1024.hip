@@ -37,6 +37,8 @@
 #include "dftL.hpp"
 #include "fpm_state.hpp"
 
+#include <algorithm>
+
 namespace fpm {
 
 namespace n1k {
@@ -44,10 +46,13 @@ constexpr int N = 1024, H = N / 2;
 constexpr int WPB = 4;             // waves (rows / columns) per block
 constexpr int NT = 64 * WPB;
 constexpr int CXP = 17;            // cross-group exchange row pitch (complex)
-constexpr int WTILE = 4 * XTILE;   // per-wave LDS: four exchange16 tiles; the
-                                   // cross-group tile (4 x 16 x CXP) fits inside
+// per-wave LDS: four half exchange16 tiles (dft16.hpp exchange16_half); the
+// cross-group exchange runs in two rounds (b = 0,1 then 2,3) through a
+// 4 x 8 x CXP tile in the same space.  Half tiles: 4.6 KB per wave instead of
+// 18 KB, so R1/R2 fit six blocks per CU instead of three.
+constexpr int WTILE = 4 * XTILE_H;
 constexpr int SPC = WPB + 1;       // column-pass strip pitch (complex)
-static_assert(4 * 16 * CXP <= WTILE, "cross-group tile");
+static_assert(4 * 8 * CXP <= WTILE, "cross-group tile");
 }  // namespace n1k
 
 namespace {
@@ -63,27 +68,34 @@ __device__ __forceinline__ float2 w1024(const float2 *twL, int e, bool inv) {
     return inv ? cconj(w) : w;
 }
 
+// cross-group tile row of (group c'', b) in round b / 2: c'' * 2 + b % 2
+__device__ __forceinline__ int xrow(int cg, int b) { return cg * 2 + (b & 1); }
+
 // layout D -> layout N.  wt: this wave's LDS tile (n1k::WTILE complex)
 template <bool INV>
 __device__ __forceinline__ void w1k_DN(float2 (&x)[16], float2 *wt, const float2 *twL, int c, int t, int xrd) {
     using namespace n1k;
     float2 y[16];
-    dft256_full<INV>(x, y, wt + c * XTILE, LdsTw{twL, t, 4}, t, xrd);   // y[r] = Y_c[t + 16 r]
-    wave_sync();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) wt[(c * 16 + r) * CXP + t] = y[r];
-    wave_sync();
+    dft256_full<INV, true>(x, y, wt + c * XTILE_H, LdsTw{twL, t, 4}, t, xrd);   // y[r] = Y_c[t + 16 r]
     const float2 *tl = fresh_lds(twL);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int kp = t + 16 * (4 * c + b);
-        float2 z[4];
-        z[0] = wt[(0 * 16 + 4 * c + b) * CXP + t];
+    for (int hb = 0; hb < 2; ++hb) {   // b = 2 hb, 2 hb + 1
+        wave_sync();
 #pragma unroll
-        for (int cc = 1; cc < 4; ++cc) z[cc] = cmul(wt[(cc * 16 + 4 * c + b) * CXP + t], w1024(tl, cc * kp, INV));
-        dft4<INV>(z);
+        for (int r = 0; r < 16; ++r)
+            if (((r & 3) >> 1) == hb) wt[(c * 8 + xrow(r >> 2, r)) * CXP + t] = y[r];   // r = 4 c'' + b
+        wave_sync();
 #pragma unroll
-        for (int p = 0; p < 4; ++p) x[4 * p + b] = z[p];
+        for (int b = 2 * hb; b < 2 * hb + 2; ++b) {
+            const int kp = t + 16 * (4 * c + b);
+            float2 z[4];
+            z[0] = wt[(0 * 8 + xrow(c, b)) * CXP + t];
+#pragma unroll
+            for (int cc = 1; cc < 4; ++cc) z[cc] = cmul(wt[(cc * 8 + xrow(c, b)) * CXP + t], w1024(tl, cc * kp, INV));
+            dft4<INV>(z);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) x[4 * p + b] = z[p];
+        }
     }
     wave_sync();  // the tile is free for the next exchange
 }
@@ -93,24 +105,28 @@ template <bool INV>
 __device__ __forceinline__ void w1k_ND(float2 (&x)[16], float2 *wt, const float2 *twL, int c, int t, int xrd) {
     using namespace n1k;
     const float2 *tl = fresh_lds(twL);
-    wave_sync();
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int kp = t + 16 * (4 * c + b);
-        float2 z[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) z[p] = x[4 * p + b];
-        dft4<INV>(z);
-        wt[(0 * 16 + 4 * c + b) * CXP + t] = z[0];
-#pragma unroll
-        for (int cc = 1; cc < 4; ++cc) wt[(cc * 16 + 4 * c + b) * CXP + t] = cmul(z[cc], w1024(tl, cc * kp, INV));
-    }
-    wave_sync();
     float2 v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = wt[(c * 16 + r) * CXP + t];     // Z_c[t + 16 r]
+    for (int hb = 0; hb < 2; ++hb) {
+        wave_sync();
+#pragma unroll
+        for (int b = 2 * hb; b < 2 * hb + 2; ++b) {
+            const int kp = t + 16 * (4 * c + b);
+            float2 z[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) z[p] = x[4 * p + b];
+            dft4<INV>(z);
+            wt[(0 * 8 + xrow(c, b)) * CXP + t] = z[0];
+#pragma unroll
+            for (int cc = 1; cc < 4; ++cc) wt[(cc * 8 + xrow(c, b)) * CXP + t] = cmul(z[cc], w1024(tl, cc * kp, INV));
+        }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (((r & 3) >> 1) == hb) v[r] = wt[(c * 8 + xrow(r >> 2, r)) * CXP + t];   // Z_c[t + 16 r]
+    }
     wave_sync();
-    dft256_full<INV>(v, x, wt + c * XTILE, LdsTw{twL, t, 4}, t, xrd);   // x[j] = X[4 (t + 16 j) + c]
+    dft256_full<INV, true>(v, x, wt + c * XTILE_H, LdsTw{twL, t, 4}, t, xrd);   // x[j] = X[4 (t + 16 j) + c]
 }
 
 __device__ __forceinline__ int fold(int k) { return k < n1k::H ? k : k - n1k::N; }  // signed frequency
@@ -126,7 +142,7 @@ __device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__re
 __global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n1k;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase(t);
+    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const float2 *twL = stage_twiddles(sm, tw);
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
@@ -149,32 +165,34 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs 
 }
 
 // C: grid (N / WPB, B), block NT
-__global__ void __launch_bounds__(n1k::NT) k_cols1024(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+__global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4))) k_cols1024(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n1k;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase(t);
+    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const float2 *twL = stage_twiddles(sm, tw);
-    float2 *strip = sm + N;            // N x SPC; the wave tiles alias it while
-    float2 *wt = strip + w * WTILE;    // every column is in registers
+    float2 *strip = sm + N;            // nb x SPC (box rows only); the wave tiles
+    float2 *wt = strip + w * WTILE;    // alias it while every column is in registers
     // XCD-aware column groups: the dispatcher deals blocks round-robin over the
     // 8 XCDs, so XCD k gets column groups k*G/8 .. (k+1)*G/8 - 1 (contiguous)
     constexpr int G = N / WPB;
     const int cg = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);
     const int r = st.r, nb = st.nb, b = blockIdx.y, x0 = cg * WPB;
     float2 *T = st.T + (size_t)b * nb * N + x0;
-    // box row j holds FFT row i = j - r mod N (:364: every other row is zero)
+    // FFT row i of a column is box row j = i + r (i <= r) or i - N + r
+    // (i >= N - r) (:364: every other row is zero)
     for (int idx = threadIdx.x; idx < nb * WPB; idx += NT) {
-        const int j = idx / WPB, cc = idx - j * WPB, i = j - r < 0 ? j - r + N : j - r;
-        strip[i * SPC + cc] = T[(size_t)j * N + cc];
+        const int j = idx / WPB, cc = idx - j * WPB;
+        strip[j * SPC + cc] = T[(size_t)j * N + cc];
     }
     __syncthreads();
+    auto boxrow = [&](int i) { return i <= r ? i + r : (i >= N - r ? i - N + r : -1); };
     float2 x[16];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
-            const int i = t + 16 * (4 * c + bb) + 256 * p;
-            x[4 * p + bb] = (i <= r || i >= N - r) ? strip[i * SPC + w] : make_float2(0.f, 0.f);
+            const int j = boxrow(t + 16 * (4 * c + bb) + 256 * p);
+            x[4 * p + bb] = j >= 0 ? strip[j * SPC + w] : make_float2(0.f, 0.f);
         }
     __syncthreads();
     w1k_ND<true>(x, wt, twL, c, t, xrd);                                 // :365 (columns)
@@ -197,13 +215,13 @@ __global__ void __launch_bounds__(n1k::NT) k_cols1024(DevState st, StepArgs sa, 
     for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
-            const int i = t + 16 * (4 * c + bb) + 256 * p;
-            if (i <= r || i >= N - r) strip[i * SPC + w] = x[4 * p + bb];
+            const int j = boxrow(t + 16 * (4 * c + bb) + 256 * p);
+            if (j >= 0) strip[j * SPC + w] = x[4 * p + bb];
         }
     __syncthreads();
     for (int idx = threadIdx.x; idx < nb * WPB; idx += NT) {
-        const int j = idx / WPB, cc = idx - j * WPB, i = j - r < 0 ? j - r + N : j - r;
-        T[(size_t)j * N + cc] = strip[i * SPC + cc];
+        const int j = idx / WPB, cc = idx - j * WPB;
+        T[(size_t)j * N + cc] = strip[j * SPC + cc];
     }
 }
 
@@ -212,7 +230,7 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     using namespace n1k;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     __shared__ float red[WPB];
-    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase(t);
+    const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const float2 *twL = stage_twiddles(sm, tw);
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
@@ -258,7 +276,7 @@ hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const
     using namespace n1k;
     if (!np1024_supported(st.np, st.r) || st.meas_g != N) return hipErrorInvalidValue;
     const size_t lds_r = (size_t)(N + WPB * WTILE) * sizeof(float2);
-    constexpr size_t strip = (size_t)N * SPC > (size_t)WPB * WTILE ? (size_t)N * SPC : (size_t)WPB * WTILE;
+    const size_t strip = std::max((size_t)st.nb * SPC, (size_t)WPB * WTILE);
     const size_t lds_c = (N + strip) * sizeof(float2);
     hipError_t e = hipFuncSetAttribute((const void *)k_cols1024, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
     if (e != hipSuccess) return e;
