@@ -23,7 +23,8 @@
 
 namespace fpm {
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
-                               const float2 *tw, hipStream_t s);
+                               const float2 *tw, bool first, hipStream_t s);
+hipError_t launch_pupil_commit(const DevState &st, hipStream_t s);
 int fft_max_len();
 int pupil_parts(int nb);
 hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const FftPlan &pl_np,
@@ -337,7 +338,10 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &st.pupil, (size_t)B * nb * nb))) return fail(rc);
     if ((rc = dalloc(c, &st.tmax, (size_t)B * st.ntx * st.nty))) return fail(rc);
     if ((rc = dalloc(c, &st.tdirty, (size_t)B * ((st.ntx * st.nty + 31) / 32)))) return fail(rc);
-    st.npart = (c->path == FPM_PATH_GENERAL) ? pupil_parts(nb) : 1;
+    // Np 1024 general path: register row/column kernels reading the stack
+    // transposed; their row IDFT writes one max|P| partial per box row
+    const bool reg1024 = c->path == FPM_PATH_GENERAL && np1024_supported(np, r) && !getenv("FPM_NO_REG1024");
+    st.npart = (c->path == FPM_PATH_GENERAL) ? (reg1024 ? std::max(pupil_parts(nb), nb) : pupil_parts(nb)) : 1;
     if ((rc = dalloc(c, &st.pmax, (size_t)B * st.npart))) return fail(rc);
     if ((rc = dalloc(c, &c->disk_dev, disk.size()))) return fail(rc);
     if ((rc = dalloc(c, &c->meas, (size_t)prob->n_stack * B * np * np))) return fail(rc);
@@ -345,8 +349,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &c->x0_dev, (size_t)prob->n_stack))) return fail(rc);
     if ((rc = dalloc(c, &c->y0_dev, (size_t)prob->n_stack))) return fail(rc);
     if (c->path == FPM_PATH_GENERAL) {
-        // Np 1024: register-resident row/column kernels reading the stack transposed
-        if (np1024_supported(np, r) && !getenv("FPM_NO_REG1024")) c->meas_g = np;
+        if (reg1024) c->meas_g = np;
         if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
@@ -497,9 +500,12 @@ namespace {
 hipError_t launch_general_iteration(fpm_ctx *c, hipStream_t s) {
     for (int i = 0; i < c->prob.n_order; ++i) {
         const int led = c->order[i];
-        hipError_t e = launch_general_step(c->st, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, s);
+        hipError_t e = launch_general_step(c->st, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0, s);
         if (e != hipSuccess) return e;
     }
+    // Np 1024: the last LED's pupil commit (the others are folded into the
+    // next LED's row IDFT)
+    if (c->meas_g == c->st.np && c->st.np == 1024) return launch_pupil_commit(c->st, s);
     return hipSuccess;
 }
 

@@ -787,17 +787,19 @@ static bool fft_fits(const FftPlan &pl, int lc, int nt = kFftThreads, int e = kF
     return true;
 }
 
-hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, hipStream_t s);
+hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, bool commit,
+                                   hipStream_t s);
 
+// first: the iteration's first LED (Np 1024: no pupil commit pending)
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
-                               const float2 *tw, hipStream_t s) {
+                               const float2 *tw, bool first, hipStream_t s) {
     StepArgs sa;
     sa.led = led;
     sa.xc = x0 + st.np / 2;
     sa.yc = y0 + st.np / 2;
     if (st.np == 1024 && st.meas_g == 1024) {
         // Np 1024: register-resident row/column transforms (np1024.hip)
-        const hipError_t e = launch_np1024_rows_cols(st, sa, tw, s);
+        const hipError_t e = launch_np1024_rows_cols(st, sa, tw, !first, s);
         if (e != hipSuccess) return e;
     } else {
         const size_t lds = 2 * (size_t)st.np * sizeof(float2);
@@ -868,6 +870,14 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<1024>), dim3(nrow, st.B), dim3(1024), ncol * sizeof(float), s, st, sa);
     else
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<256>), dim3(nrow, st.B), dim3(256), ncol * sizeof(float), s, st, sa);
+    // Np 1024: the commit is folded into the next LED's row IDFT (np1024.hip)
+    // and runs here only after the iteration's last LED (launch_pupil_commit)
+    if (!(st.np == 1024 && st.meas_g == 1024))
+        hipLaunchKernelGGL(k_pupil_commit, dim3(st.npart, st.B), dim3(kCommitThreads), 0, s, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_pupil_commit(const DevState &st, hipStream_t s) {
     hipLaunchKernelGGL(k_pupil_commit, dim3(st.npart, st.B), dim3(kCommitThreads), 0, s, st);
     return hipGetLastError();
 }

@@ -138,24 +138,53 @@ __device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__re
     return sm;
 }
 
-// R1: grid (ceil(nb / WPB), B), block NT
-__global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+// R1: grid (ceil(nb / WPB), B), block NT.  Also the previous LED's pupil
+// commit (general.hip K5, folded in when `commit`): P += dP / max|objF| on
+// this row's disk pixels (:468-475), with max|objF| from the tile-row maxima
+// K4 left (:460,467), and the row's max|P| for this LED's update (:415) as
+// partial pmax[row] -- the same arithmetic as K5, so the results are
+// bit-identical; K5 itself then runs once, after the last LED.
+__global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw,
+                                                          int commit) {
     using namespace n1k;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    __shared__ float red[WPB];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
+    const int lane = threadIdx.x & 63;
     const float2 *twL = stage_twiddles(sm, tw);
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
+    float omax = 1.f;
+    if (commit) {  // block-uniform
+        float m = 0.f;
+        for (int i = threadIdx.x; i < st.nty; i += NT) m = fmaxf(m, st.rmax[(size_t)b * st.nty + i]);
+        omax = block_max(m, red);
+    }
     if (row >= nb) return;  // wave-uniform; no block barrier follows
     const int ky = row - r, w2 = r * r - ky * ky;
-    const float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;   // indexed by kx
+    float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;         // indexed by kx
+    const float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;         // + kx (:358-362)
     float2 x[16];
+    float pmx = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int kx = fold(4 * (t + 16 * j) + c);
-        x[j] = kx * kx <= w2 ? cmul(spec_ld(st, b, srow + kx), pup[kx]) : make_float2(0.f, 0.f);  // :364
+        x[j] = make_float2(0.f, 0.f);
+        if (kx * kx <= w2) {
+            float2 p = pup[kx];
+            if (commit) {
+                const float2 d = dP[kx];
+                p.x += d.x / omax;
+                p.y += d.y / omax;
+                pup[kx] = p;
+            }
+            pmx = fmaxf(pmx, cmag(p));
+            x[j] = cmul(spec_ld(st, b, srow + kx), p);  // :364
+        }
     }
+    pmx = wave_max(pmx);
+    if (lane == 0) st.pmax[(size_t)b * st.npart + row] = pmx;
     w1k_DN<true>(x, wt, twL, c, t, xrd);                                 // :365 (rows)
     float2 *T = st.T + ((size_t)b * nb + row) * N + t + 64 * c;
 #pragma unroll
@@ -272,16 +301,17 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
 // layout (the caller permutes it when this returns true).
 bool np1024_supported(int np, int r) { return np == n1k::N && r >= 1 && r < n1k::H; }
 
-hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, hipStream_t s) {
+hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, bool commit,
+                                   hipStream_t s) {
     using namespace n1k;
-    if (!np1024_supported(st.np, st.r) || st.meas_g != N) return hipErrorInvalidValue;
+    if (!np1024_supported(st.np, st.r) || st.meas_g != N || st.npart < st.nb) return hipErrorInvalidValue;
     const size_t lds_r = (size_t)(N + WPB * WTILE) * sizeof(float2);
     const size_t strip = std::max((size_t)st.nb * SPC, (size_t)WPB * WTILE);
     const size_t lds_c = (N + strip) * sizeof(float2);
     hipError_t e = hipFuncSetAttribute((const void *)k_cols1024, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
     if (e != hipSuccess) return e;
     const dim3 rgrid((st.nb + WPB - 1) / WPB, st.B);
-    hipLaunchKernelGGL(k_rows1024_inv, rgrid, dim3(NT), lds_r, s, st, sa, tw);
+    hipLaunchKernelGGL(k_rows1024_inv, rgrid, dim3(NT), lds_r, s, st, sa, tw, commit ? 1 : 0);
     hipLaunchKernelGGL(k_cols1024, dim3(N / WPB, st.B), dim3(NT), lds_c, s, st, sa, tw);
     hipLaunchKernelGGL(k_rows1024_fwd, rgrid, dim3(NT), lds_r, s, st, sa, tw);
     return hipGetLastError();
