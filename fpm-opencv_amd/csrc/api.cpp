@@ -605,7 +605,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         const double steps = (double)iters * c->prob.n_order * c->st.B;
         const char *names[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre", "max",
                                       "P",      "A:rowIDFT",   "C:rowDFT",  "upd:body",    "B:loop",
-                                      "split:stores", "split:publish"};
+                                      "split:Fstores", "split:Fwait"};
         for (int v = 0; v < 2; ++v) {
             fprintf(stderr, "[fpm stamps] cycles per LED step (%s wave view, mean over blocks):", v ? "last" : "first");
             for (int i = 0; i < kStamps; ++i) fprintf(stderr, " %s=%.0f", names[i], h[v * kStamps + i] / steps);

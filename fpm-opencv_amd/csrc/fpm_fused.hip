@@ -78,16 +78,18 @@ struct FusedArgs {
     // split mode (NT 512, B <= CUs / 2): two workgroups per patch, half h of the
     // columns each (split_layout); handoffs through xch with device-scope flags
     int split;
-    float2 *xch;                // [B][kXchPatch]: F partial | tail F partial | P | tail P
-    int *flags;                 // [B][2]: F partial of LED it ready (it + 1), P + spectrum of LED it (it + 1);
+    float2 *xch;                // [B][2 halves][2 LED parities][kXchHalf]: F partial | tail F partial
+    int *flags;                 // [B][2]: half h's F partials of LED it published (it + 1);
                                 // then the abort flag, then [B][2] XCC_ID + 1 of each half
     int *abort_flag;            // a handoff timed out: every workgroup leaves
 };
 
-// split-mode exchange area per patch (float2): F partials and P of the 512
-// lanes (12 slots each, lane-major) and of the <= 64 tail pixels
-constexpr int kXchF = 0, kXchTF = 12 * 512, kXchP = kXchTF + 64, kXchTP = kXchP + 12 * 512;
-constexpr int kXchPatch = kXchTP + 64;
+// split-mode exchange area per patch (float2): each half's F partials of the
+// 512 lanes (12 slots each, lane-major) and of the <= 64 tail pixels, double
+// buffered by LED parity (a half overwrites its LED-i buffer only at LED i+2,
+// after the partner has published LED i+1, i.e. has read LED i's partials)
+constexpr int kXchTF = 12 * 512, kXchHalf = kXchTF + 64;
+constexpr int kXchPatch = 4 * kXchHalf;
 
 // Handoff between the two workgroups of a patch (split mode).  Everything the
 // partner reads -- the exchange area, the updated spectrum window, the flags --
@@ -318,7 +320,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     bool local = false;
     // (descriptors are built unconditionally: the type has no empty state)
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(xch, 0, split ? kXchPatch * (int)sizeof(float2) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(spec, 0, split ? L * L * (int)sizeof(float2) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, split ? 2 * (int)sizeof(int) : 0, 0x00020000);
     if (split) {
         if (tid == 0) {
@@ -360,18 +361,10 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                           : __builtin_amdgcn_raw_buffer_load_b64(rx, lane_off, slot * (int)sizeof(float2),
                                                                  (int)(16u | (1u << 31))));
     };
-    auto sst = [&](float2 *p, float2 v) {
-        if (!split || local) *p = v;
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
-                                                  (int)(p - spec) * (int)sizeof(float2), 0, 16);
-    };
-    auto sld = [&](const float2 *p) {
-        const int off = (int)(p - spec) * (int)sizeof(float2);
-        return __builtin_bit_cast(float2, local ? __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, kAuxL2Volatile)
-                                                : __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0,
-                                                                                       (int)(16u | (1u << 31))));
-    };
+    // spectrum stores: in split mode both halves run the identical update and
+    // write identical values, and each reads back only its own writes (the
+    // next window, the dirty-tile re-scan), so plain stores serve both
+    auto sst = [&](float2 *p, float2 v) { *p = v; };
     const float epsn = st.eps * (float)(NP * NP);  // eps on the unscaled IDFT
     const float epsn_im = st.eps_im * (float)(NP * NP);
     __syncthreads();
@@ -640,43 +633,37 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             __syncthreads();  // half-T reusable; tailF
             FPM_STAMP(3)
         }
-        if (split && hown == 1) {
-            // second half's workgroup: hand its F partials to the first, then wait
-            // for the updated spectrum and pupil of this LED before the next one
+        if (split) {
+            // symmetric handoff: publish this half's F partials, take the
+            // partner's, and both halves run the same update (bit-identical:
+            // the sum is F_0 + F_1 in both, cadd commutes exactly); one handoff
+            // per LED, and no half waits for the other's update
+            const int par = it & 1;
+            const int mine = (hown * 2 + par) * kXchHalf, other = ((1 - hown) * 2 + par) * kXchHalf;
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) xst(kXchF + (j * 6 + s) * NT, F[j][s]);
-            if (tid < a.n_tail_px) xst(kXchTF, tailF[tid]);
-            handoff_publish(flg, it + 1, local);
-            FPM_STAMP(9)  // (split, second half: the publish)
-            if (it + 1 >= a.n_order) break;
-            if (!handoff_wait(flg + 1, it + 1, a.abort_flag, ccnt + 1, local, rf, (int)sizeof(int))) break;
-#pragma unroll
-            for (int j = 0; j < RPG; ++j)
-#pragma unroll
-                for (int s = 0; s < 6; ++s) P[j][s] = xld(kXchP + (j * 6 + s) * NT);
-            if (towner) Pt = xld(kXchTP);
-            const float2 *sr = window(it + 1);  // written by the partner: coherent loads
-#pragma unroll
-            for (int j = 0; j < RPG; ++j)
-#pragma unroll
-                for (int s = 0; s < 6; ++s)
-                    Opre[j][s] = ((inmask[j] >> s) & 1) ? sld(sr + (kyr[j] * L + t) + soff(s)) : make_float2(0.f, 0.f);
-            if (towner) Ot = sld(sr + tp.x * L + tp.y);
-            FPM_STAMP(4)  // (split, second half: the wait for the partner and the reloads)
-            continue;
-        }
-        if (split) {  // first half's workgroup: add the second half's F partials
-            if (!handoff_wait(flg, it + 1, a.abort_flag, ccnt + 1, local, rf, 0)) {
+                for (int s = 0; s < 6; ++s) xst(mine + (j * 6 + s) * NT, F[j][s]);
+            if (tid < a.n_tail_px) xst(mine + kXchTF, tailF[tid]);
+            FPM_STAMP(11)
+            handoff_publish(flg + hown, it + 1, local);
+            if (!handoff_wait(flg + 1 - hown, it + 1, a.abort_flag, ccnt + 1, local, rf,
+                              (1 - hown) * (int)sizeof(int))) {
                 aborted = true;
                 break;
             }
+            FPM_STAMP(12)
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) F[j][s] = cadd(F[j][s], xld(kXchF + (j * 6 + s) * NT));
-            if (tid < a.n_tail_px) tailF[tid] = cadd(tailF[tid], xld(kXchTF));
+                for (int s = 0; s < 6; ++s) {
+                    const float2 o = xld(other + (j * 6 + s) * NT);
+                    F[j][s] = hown == 0 ? cadd(F[j][s], o) : cadd(o, F[j][s]);
+                }
+            if (tid < a.n_tail_px) {
+                const float2 o = xld(other + kXchTF);
+                tailF[tid] = hown == 0 ? cadd(tailF[tid], o) : cadd(o, tailF[tid]);
+            }
         }
 
         // ---- object update on the support (:405-447) and pupil numerator (:457-464).
@@ -813,16 +800,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
         pm = sqrtf(pm2);
         FPM_STAMP(6)
-        if (split && it + 1 < a.n_order) {  // spectrum (written above) and P for the partner
-#pragma unroll
-            for (int j = 0; j < RPG; ++j)
-#pragma unroll
-                for (int s = 0; s < 6; ++s) xst(kXchP + (j * 6 + s) * NT, P[j][s]);
-            if (towner) xst(kXchTP, Pt);
-            FPM_STAMP(11)
-            handoff_publish(flg + 1, it + 1, local);
-            FPM_STAMP(12)
-        }
         (void)aborted;
     }
 #undef FPM_STAMP

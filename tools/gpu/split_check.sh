@@ -11,3 +11,5 @@ tail -1 $O/tests.log
 timeout -k 10 300 python bench.py --patches-total 128 --steps 3 --warmup 1 --no-cpu-baseline > $O/c4_shard128.json 2> $O/c4s.err || { echo "c4 shard rc=$?"; tail $O/c4s.err; exit 1; }
 FPM_NO_SPLIT=1 timeout -k 10 300 python bench.py --patches-total 128 --steps 3 --warmup 1 --no-cpu-baseline > $O/c4_shard128_nosplit.json 2> $O/c4n.err || { echo "c4 nosplit rc=$?"; tail $O/c4n.err; exit 1; }
 for f in c4_shard128 c4_shard128_nosplit; do python3 -c "import json; d=json.load(open('$O/$f.json')); print('$f', d['value'], d['ms_per_step'], d['led_ms_per_step'], d['objcrop_ms_per_step'])"; done
+FPM_STAMPS=1 timeout -k 10 240 python bench.py --patches-total 128 --steps 1 --warmup 0 --no-cpu-baseline 2>&1 >/dev/null | grep "fpm stamps" > $O/split_stamps.txt || true
+cat $O/split_stamps.txt
