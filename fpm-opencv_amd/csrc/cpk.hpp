@@ -28,6 +28,26 @@ typedef float pf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ pf2 pin(float2 a) { return __builtin_bit_cast(pf2, a); }
 __device__ __forceinline__ float2 pout(pf2 a) { return __builtin_bit_cast(float2, a); }
 
+// Amplitude-replacement scale sqrt(I) / sqrt(mag2) (fpmMain.cpp:378-394, with
+// mag2 = |psi + eps (1 + i)|^2 on the unscaled transform) for an integer
+// measurement I >= 0: I * rsq(mag2 I + FLT_MIN), ONE transcendental (v_rsq_f32
+// issues in 8 cycles, a plain VALU op in 4; MI355X_MICROARCH.md constants
+// table) where rsq(mag2 * rcp(I)) needed two; the fma costs what the mul did.
+// FLT_MIN keeps I = 0 finite: 0 * rsq(FLT_MIN) = 0, the reference's sqrt(0)
+// factor (it is below the rounding of mag2 I for any I >= 1 and mag2 the
+// solver meets).  -DFPM_AMP_RCP builds the two-transcendental form for A/B runs.
+__device__ __forceinline__ float amp_scale(float mag2, float I) {
+#ifdef FPM_AMP_RCP
+    return __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(I));
+#elif defined(FPM_AMP_NANTEST)  // TEMP diagnostic
+    float s;
+    asm("v_mul_legacy_f32 %0, %1, %2" : "=v"(s) : "v"(I), "v"(__builtin_amdgcn_rsqf(mag2 * I)));
+    return s;
+#else
+    return I * __builtin_amdgcn_rsqf(__builtin_fmaf(mag2, I, 1.17549435e-38f));
+#endif
+}
+
 // a + W4 b with W4 = -i (forward) or +i (inverse):
 //   -i b = (b.y, -b.x) -> (a.x + b.y, a.y - b.x);  +i b = (-b.y, b.x) -> (a.x - b.y, a.y + b.x)
 // op_sel / op_sel_hi pick b.y for the low lane and b.x for the high lane.

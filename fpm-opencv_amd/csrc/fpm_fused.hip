@@ -315,6 +315,14 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
     float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
     float pm = st.pmax[b];
+    // max|P| = sqrt of the per-wave maxima of |P|^2 the pupil phase leaves in red[32..]
+    auto pm_of_red = [&]() {
+        float pm2 = red[32];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
+        return sqrtf(pm2);
+    };
+    bool pupil_done = false;  // red[32..] holds a pupil phase's maxima
     // split mode: learn whether the partner shares this XCD (then L2-level
     // handoffs, see ld_l2) -- one coherent exchange per launch
     bool local = false;
@@ -402,6 +410,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(sr, j, s);
         if (towner) Ot = sr[tp.x * L + tp.y];
     }
+#ifdef FPM_PRIO_YOUNG  // A/B: static VALU priority for the second-dispatched half of the waves
+    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
@@ -554,7 +565,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     // 1/I = +inf and a zero scale, the reference's sqrt(0) factor
                     const pf2 tt = pin(r[m2]) + (pf2){epsn, epsn_im};
                     const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
-                    const float sc = __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(Iv));
+                    const float sc = amp_scale(mag2, Iv);
                     v[m2] = pout(pin(r[m2]) * sc);
                 }
                 float2 o[6];
@@ -681,6 +692,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
+        if (it > 0) pm = pm_of_red();  // the previous LED's pupil (:415)
         loadP();
         // Straight-line over all slots: outside the support O = P = 0, so the
         // numerator is exactly 0 and only the spectrum store and the tile
@@ -791,18 +803,19 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         // red[32..47] is not used by the max phase, so no barrier is needed
         // before writing it; nothing read below is rewritten by another
         // thread before the next LED's first barrier (numerators sit in this
-        // thread's own half-T slots, tailX was last read in pass A)
+        // thread's own half-T slots, tailX was last read in pass A).
+        // max|P| is first needed by the next LED's object update, several
+        // barriers later: it is reduced there (pm_of_red), not behind a
+        // barrier of its own here.
         pmx = wave_max(pmx);
         if (lane == 0) red[32 + w] = pmx;
-        __syncthreads();
-        float pm2 = red[32];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
-        pm = sqrtf(pm2);
+        pupil_done = true;
         FPM_STAMP(6)
         (void)aborted;
     }
 #undef FPM_STAMP
+    __syncthreads();  // the last LED's red[32..]
+    if (pupil_done) pm = pm_of_red();
     // stamps of the first and the last wave (the barrier waits show who is slow)
     // (split mode: the first wave of each half's workgroup)
     if (a.dbg && (split ? tid == 0 : (tid == 0 || tid == NT - 64)))

@@ -215,11 +215,10 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
             for (int k = 0; k < 20; ++k) {
                 // psi = r/Np^2 (:365); sqrt(I) psi/|psi + eps| = r / sqrt(|r + eps Np^2|^2 / I)
-                const float invI = __builtin_amdgcn_rcpf(
-                    (float)((k & 1) ? (iw[k >> 1] >> 16) : (iw[k >> 1] & 0xffffu)));
+                const float Iv = (float)((k & 1) ? (iw[k >> 1] >> 16) : (iw[k >> 1] & 0xffffu));
                 const pf2 tt = pin(v[k]) + (pf2){epsn, epsn_im};
                 const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
-                const float sc = __builtin_amdgcn_rsqf(mag2 * invI);
+                const float sc = amp_scale(mag2, Iv);
                 v[k] = pout(pin(v[k]) * sc);
             }
             dft200<false, false>(v, tile, tw2, l, xrd);

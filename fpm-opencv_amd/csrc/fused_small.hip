@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                 const pf2 r = pin(col[e]);
                 const pf2 tt = r + (pf2){epsn, epsn_im};
                 const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
-                col[e] = pout(r * __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(Iv)));
+                col[e] = pout(r * amp_scale(mag2, Iv));
             }
             __syncthreads();
             FPM_STAMP(2)
@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             const pf2 r = pin(col[e]);
             const pf2 tt = r + (pf2){epsn, epsn_im};
             const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
-            col[e] = pout(r * __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(Iv)));
+            col[e] = pout(r * amp_scale(mag2, Iv));
         }
         __syncthreads();
         FPM_STAMP(2)

@@ -34,6 +34,7 @@
 //     X[4 m + c] = sum_k' W256^{k' m} W1024^{k' c} sum_p x[k' + 256 p] W4^{p c}.
 #include <hip/hip_runtime.h>
 
+#include "cpk.hpp"
 #include "dftL.hpp"
 #include "fpm_state.hpp"
 
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
         const float iv = (float)Ic[4 * (t + 16 * j)];
         const float2 v = x[j];
         const float tr = v.x + epsn, ti = v.y + epsn_im;
-        const float s = __builtin_amdgcn_rsqf(__builtin_fmaf(tr, tr, ti * ti) * __builtin_amdgcn_rcpf(iv));
+        const float s = amp_scale(__builtin_fmaf(tr, tr, ti * ti), iv);
         x[j] = make_float2(v.x * s, v.y * s);
     }
     w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (columns)

@@ -112,11 +112,15 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
         // objF row y + h H is spec row y + (1 - h) H: the live rows of this
         // half are the contiguous range [ya, yb]
         const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
-        // strip load: consecutive threads take consecutive columns of a row
+        // strip load: consecutive threads take consecutive column pairs of a row
+        // (16-byte loads: twice the bytes in flight per load instruction)
+        constexpr int G2 = G / 2;
 FPM_CROP_PRAGMA_UNROLL
-        for (int idx = ya * G + threadIdx.x; idx < (yb + 1) * G; idx += NTH) {
-            const int y = idx / G, cc = idx - y * G;
-            strip[y * SP + cc] = base[(size_t)(y + h * H) * L + cc];
+        for (int idx = ya * G2 + threadIdx.x; idx < (yb + 1) * G2; idx += NTH) {
+            const int y = idx / G2, cc = 2 * (idx - y * G2);
+            const float4 q = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
+            strip[y * SP + cc] = make_float2(q.x, q.y);
+            strip[y * SP + cc + 1] = make_float2(q.z, q.w);
         }
         __syncthreads();
 #pragma unroll
@@ -140,9 +144,10 @@ FPM_CROP_PRAGMA_UNROLL
                     strip[(t + 16 * r + 256 * p - h * H) * SP + g] = cscale(x[p][r], scale);
         __syncthreads();
 FPM_CROP_PRAGMA_UNROLL
-        for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
-            const int y = idx / G, cc = idx - y * G;
-            base[(size_t)(y + h * H) * L + cc] = strip[y * SP + cc];
+        for (int idx = threadIdx.x; idx < H * G / 2; idx += NTH) {
+            const int y = idx / (G / 2), cc = 2 * (idx - y * (G / 2));
+            const float2 p0 = strip[y * SP + cc], p1 = strip[y * SP + cc + 1];
+            *(float4 *)(base + (size_t)(y + h * H) * L + cc) = make_float4(p0.x, p0.y, p1.x, p1.y);
         }
     }
 }
