@@ -39,10 +39,6 @@ __device__ __forceinline__ float2 pout(pf2 a) { return __builtin_bit_cast(float2
 __device__ __forceinline__ float amp_scale(float mag2, float I) {
 #ifdef FPM_AMP_RCP
     return __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(I));
-#elif defined(FPM_AMP_NANTEST)  // TEMP diagnostic
-    float s;
-    asm("v_mul_legacy_f32 %0, %1, %2" : "=v"(s) : "v"(I), "v"(__builtin_amdgcn_rsqf(mag2 * I)));
-    return s;
 #else
     return I * __builtin_amdgcn_rsqf(__builtin_fmaf(mag2, I, 1.17549435e-38f));
 #endif

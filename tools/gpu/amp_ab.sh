@@ -24,5 +24,6 @@ for v in default ${VARIANTS}; do
   timeout -k 10 300 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline > $O/c3_$v.json 2> $O/c3_$v.err || { echo "c3 $v rc=$?"; tail $O/c3_$v.err; exit 1; }
   timeout -k 10 300 python bench.py --config c2 --steps 5 --warmup 1 --no-cpu-baseline > $O/c2_$v.json 2> $O/c2_$v.err || { echo "c2 $v rc=$?"; tail $O/c2_$v.err; exit 1; }
   fi
-  for f in m ${ONLY_M:+x} ${ONLY_M:-c3 c2}; do [ $f = x ] && continue; python3 -c "import json; d=json.load(open('$O/${f}_$v.json')); print('$v $f', d['value'], d['ms_per_step'], d.get('led_ms_per_step'), d.get('objcrop_ms_per_step'))"; done
+  FS="m c3 c2"; [ -n "$ONLY_M" ] && FS=m
+  for f in $FS; do python3 -c "import json; d=json.load(open('$O/${f}_$v.json')); print('$v $f', d['value'], d['ms_per_step'], d.get('led_ms_per_step'), d.get('objcrop_ms_per_step'))"; done
 done
