@@ -147,6 +147,76 @@ def load_pmc(path, kernel):
             f"{os.path.basename(path)} (csrc {d['src_hash']})")
 
 
+def kernel_name(info):
+    """Name of the LED-update kernel the context launches (rocprof / pmc key):
+    the template instance for the Np 256 kernel (workgroups per patch)."""
+    import fpm_amd
+    if info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256:
+        return f"k_fused_iteration<512,{info.wg_per_patch}>"
+    return fpm_amd.KERNEL_NAMES[info.fused_kernel]
+
+
+def default_pmc(args, info):
+    """Counter profile of this workload's kernel (tools/gpu/prof_counters.sh
+    writes one per workload: profiles/pmc_<config>_<kernel>.json)."""
+    k = kernel_name(info).replace("<", "_").replace(">", "").replace(",", "_")
+    return os.path.join(ROOT, "profiles", f"pmc_{args.config}_{k}.json")
+
+
+def fp32_roof_updates_per_s(np_, nb, support_px):
+    """LED-updates/s at the FP32 peak: the ceiling of a compute-bound kernel
+    on the algorithmic flop model (7.61 MFLOP at the metric)."""
+    return F32_PEAK_TFLOPS * 1e12 / algorithmic_flops_per_update(np_, nb, support_px)
+
+
+def roofline_line(geo, info, per_launch_ms, per_launch_updates, pmc_path):
+    """roofline object of the bench line for the context's LED-update kernel.
+
+    The fused kernels keep T in LDS and P in registers: they move the
+    measurement plus the spectrum on the support (1.02x that by counters at
+    the metric), so the HBM roof is far away and what binds is FP32 VALU issue
+    (SQ counters in `counters`).  `bound` is therefore "valu": `achieved` is
+    the algorithmic flop rate (support-pruned transform model) against the
+    157.3 TFLOP/s FP32 peak.  The HBM view (minimum bytes, SURVEY.md 8(d)'s
+    support-restricted 2 Np^2 + 32 |S| and dense 34 Np^2 figures) sits in
+    `hbm`; `ceiling` states what the north-star '>= 70 % of HBM' target maps
+    to on this kernel (the FP32 roof reached first)."""
+    np_, S = geo["np_"], info.support_px
+    t = per_launch_ms * 1e-3
+    kname = kernel_name(info)
+    traffic, counters, pmc_note = load_pmc(pmc_path, kname)
+    flops = algorithmic_flops_per_update(np_, info.box, S) * per_launch_updates
+    achieved_tf = flops / t / 1e12
+    min_bytes = min_bytes_per_update(np_, S) * per_launch_updates
+    sup_bytes = (2.0 * np_ * np_ + 32.0 * S) * per_launch_updates
+    dense_bytes = dense_bytes_per_update(np_) * per_launch_updates
+    roof_u = fp32_roof_updates_per_s(np_, info.box, S)
+    hbm = dict(achieved=round(min_bytes / t / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+               frac=round(min_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
+               bytes_model=f"2*Np^2 (uint16 I) + 16*|S| (O read+write on the {S}-px support) per LED-update "
+                           f"x {per_launch_updates} LED-updates per launch",
+               algorithmic_bytes_per_launch=min_bytes,
+               support_restricted_frac=round(sup_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
+               support_restricted_note="SURVEY.md 8(d): 2*Np^2 + 32*|S| B per LED-update",
+               dense_equivalent_frac=round(dense_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
+               dense_note="SURVEY.md 8(d) dense 34*Np^2 definition; bytes this design never moves",
+               measured_GBs=(round(traffic / t / 1e9, 1) if traffic else None),
+               traffic_over_algorithmic=(round(traffic / min_bytes, 3) if traffic else None))
+    return dict(bound="valu", achieved=round(achieved_tf, 2), peak=F32_PEAK_TFLOPS, unit="TFLOP/s",
+                frac=round(achieved_tf / F32_PEAK_TFLOPS, 4), traffic=traffic,
+                kernel=kname, launch_ms=round(per_launch_ms, 4),
+                flops_model=f"5 N log2 N per executed pruned 1-D DFT (nb={info.box} row IDFTs + Np column "
+                            f"IDFT/DFT pairs + nb row DFTs) + 12 flop/px amplitude + 60 flop per support px, "
+                            f"x {per_launch_updates} LED-updates per launch",
+                algorithmic_flops_per_launch=flops,
+                hbm=hbm,
+                ceiling=dict(fp32_roof_led_updates_per_s=round(roof_u, 1),
+                             hbm_frac_at_fp32_roof=round(roof_u * min_bytes_per_update(np_, S) / 1e9 / HBM_PEAK_GBS, 4),
+                             note="north_star asks >= 70 % of the HBM roof; on the minimum bytes that needs "
+                                  "more flops than the FP32 peak, so the FP32 roof is the reachable ceiling"),
+                traffic_source=pmc_note, counters=counters)
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -243,7 +313,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this job may use (host_cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--pmc", default="", help="counter profile (tools/pmc_to_json.py); default: the workload's "
+                                              "profiles/pmc_<config>_<kernel>.json")
     ap.add_argument("--pcie", action="store_true",
                     help="also time the host->device stack upload (fpm_upload_stack from host memory); "
                          "reported beside the line as upload, never in value")
@@ -252,6 +323,23 @@ def main():
     ap.add_argument("--data", default="model", choices=["model", "random"],
                     help="random: uniform uint16 stack (profiling runs only; not a bench number)")
     args = ap.parse_args()
+
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start one rank per GPU under
+        # torch.distributed.run as a CHILD process (nothing here has touched
+        # the GPU yet) and exit with its status -- never a 1-GPU number
+        # labelled as N
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        raise SystemExit(subprocess.call(cmd))
+    if world_env is not None and int(world_env) != args.gpus and "--gpus" in " ".join(sys.argv):
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world_env}: launch one rank per GPU")
 
     import numpy as np
     import torch
@@ -343,38 +431,9 @@ def main():
     updates = (args.patches_total if strong else B * world) * geo["n_led"] * args.steps
     value = updates / elapsed
     per_launch_ms = led_ms / max(launches, 1)
-    per_launch_updates = B * geo["n_led"] if info.path == fpm_amd.PATH_FUSED else B
-    flops = algorithmic_flops_per_update(geo["np_"], info.box, info.support_px) * per_launch_updates
-    achieved_tf = flops / (per_launch_ms * 1e-3) / 1e12
-    kname = "k_fused_iteration" if info.path == fpm_amd.PATH_FUSED else "general_led_step(4 kernels)"
-    traffic, counters, pmc_note = load_pmc(args.pmc, kname)
-    # Headline roofline: HBM against the MINIMUM bytes of the support-pruned
-    # step (uint16 I + spectrum O read/write on the support, per LED-update).
-    # The kernel's binding resource is FP32 issue (`compute`); SURVEY.md
-    # 8(d)'s dense 34 Np^2 definition is kept as a labelled dense-equivalent.
-    min_bytes = min_bytes_per_update(geo["np_"], info.support_px) * per_launch_updates
-    achieved_gbs = min_bytes / (per_launch_ms * 1e-3) / 1e9
-    dense_bytes = dense_bytes_per_update(geo["np_"]) * per_launch_updates
-    dense_gbs = dense_bytes / (per_launch_ms * 1e-3) / 1e9
-    roofline = dict(bound="hbm", achieved=round(achieved_gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved_gbs / HBM_PEAK_GBS, 4), traffic=traffic,
-                    kernel=kname, launch_ms=round(per_launch_ms, 4),
-                    algorithmic_bytes_per_launch=min_bytes,
-                    bytes_model=f"2*Np^2 (uint16 I) + 16*|S| (O read+write on the {info.support_px}-px support) "
-                                f"per LED-update x {per_launch_updates} LED-updates per launch",
-                    measured_hbm_GBs=(round(traffic / (per_launch_ms * 1e-3) / 1e9, 1) if traffic else None),
-                    traffic_over_algorithmic=(round(traffic / min_bytes, 3) if traffic else None),
-                    traffic_source=pmc_note,
-                    dense_equivalent=dict(bytes_per_update=dense_bytes_per_update(geo["np_"]),
-                                          GBs=round(dense_gbs, 1), frac_of_peak=round(dense_gbs / HBM_PEAK_GBS, 4),
-                                          note="SURVEY.md 8(d) dense 34*Np^2 definition; not bytes moved"),
-                    compute=dict(bound="fp32 VALU issue", peak_TFLOPs=F32_PEAK_TFLOPS,
-                                 dense_equivalent_TFLOPs=round(dense_flops_per_update(geo["np_"]) * per_launch_updates
-                                                               / (per_launch_ms * 1e-3) / 1e12, 2),
-                                 executed_TFLOPs=round(achieved_tf, 2),
-                                 executed_frac=round(achieved_tf / F32_PEAK_TFLOPS, 4),
-                                 executed_flops_per_launch=flops),
-                    counters=counters)
+    fused = info.path == fpm_amd.PATH_FUSED
+    per_launch_updates = B * geo["n_led"] if fused else B
+    roofline = roofline_line(geo, info, per_launch_ms, per_launch_updates, args.pmc or default_pmc(args, info))
 
     gather = None
     if (world > 1 or strong) and not args.no_gather:
@@ -446,6 +505,7 @@ def main():
                        **({"patches_total": args.patches_total} if strong else {}),
                        "nlarge": int(geo["L"]), "na_radius": int(geo["r"]),
                        "path": "fused" if info.path == fpm_amd.PATH_FUSED else "general",
+                       "kernel": kernel_name(info), "workgroups_per_patch": int(info.wg_per_patch),
                        "parallelism": f"patch-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,

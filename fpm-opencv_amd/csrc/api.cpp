@@ -48,10 +48,11 @@ bool np1024_supported(int np, int r);
 size_t fused_park_elems(int nt, int B);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  float2 *pscr, int nt, unsigned long long *dbg, float2 *xch, int *flags,
+                                  float2 *pscr, int nt, int ks, unsigned long long *dbg, float2 *xch, int *flags,
                                   hipStream_t s);
-size_t fused_xch_elems(int B);
-bool fused_split_wanted(int nt, int B, int n_cu);
+size_t fused_xch_elems(int B, int ks);
+size_t fused_flag_words(int B, int ks);
+int fused_split_parts(int nt, int B, int n_cu);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
@@ -127,8 +128,9 @@ struct fpm_ctx {
                                     // kernel and the Np 1024 general path, transposed); 0: C-ABI
     float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
     int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
-    float2 *xch = nullptr;          // split mode (two workgroups per patch): exchange area
-    int *split_flags = nullptr;     //   handoff flags [2B] + abort flag
+    int split_ks = 1;               // split mode: workgroups per patch (2 or 4), else 1
+    float2 *xch = nullptr;          //   exchange area
+    int *split_flags = nullptr;     //   handoff flags [KS B] + sticky abort flag + XCC ids [KS B]
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
@@ -360,9 +362,13 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         int n_cu = 0, coop = 0;
         (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
         (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device);
-        if (c->fused_nt && coop && fused_split_wanted(c->fused_nt, B, n_cu)) {
-            if ((rc = dalloc(c, &c->xch, fused_xch_elems(B)))) return fail(rc);
-            if ((rc = dalloc(c, &c->split_flags, 4 * (size_t)B + 1))) return fail(rc);
+        c->split_ks = (c->fused_nt && coop) ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
+        if (c->split_ks > 1) {
+            if ((rc = dalloc(c, &c->xch, fused_xch_elems(B, c->split_ks)))) return fail(rc);
+            const size_t nf = fused_flag_words(B, c->split_ks);
+            if ((rc = dalloc(c, &c->split_flags, nf))) return fail(rc);
+            if (hipMemset(c->split_flags, 0, nf * sizeof(int)) != hipSuccess)
+                return fail(set_err(FPM_ERR_DEVICE, "memset failed"));
         }
     }
     st.meas = c->meas;
@@ -563,8 +569,8 @@ int fpm_run(fpm_ctx *c, int iters) {
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
-                                           c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->dbg,
-                                           c->xch, c->split_flags, c->stream));
+                                           c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->split_ks,
+                                           c->dbg, c->xch, c->split_flags, c->stream));
         } else if (use_graph) {
             HIP_TRY(hipGraphLaunch(c->led_graph_exec, c->stream));
         } else {
@@ -579,10 +585,21 @@ int fpm_run(fpm_ctx *c, int iters) {
     }
     HIP_TRY(hipEventRecord(ev[need - 1], c->stream));
     HIP_TRY(hipEventSynchronize(ev[need - 1]));
-    if (c->split_flags) {  // a split-mode handoff that timed out leaves the results undefined
+    if (c->split_flags) {
+        // a split-mode handoff that timed out in ANY iteration leaves the
+        // results undefined: the abort word is sticky across launches; report
+        // it, clear it, and require a fresh fpm_init before the next run
         int ab = 0;
-        HIP_TRY(hipMemcpy(&ab, c->split_flags + 2 * (size_t)c->st.B, sizeof(int), hipMemcpyDeviceToHost));
-        if (ab) return set_err(FPM_ERR_DEVICE, "split-mode handoff between the two workgroups of a patch timed out");
+        int *abw = c->split_flags + (size_t)c->split_ks * c->st.B;
+        HIP_TRY(hipMemcpy(&ab, abw, sizeof(int), hipMemcpyDeviceToHost));
+        if (ab) {
+            HIP_TRY(hipMemset(abw, 0, sizeof(int)));
+            c->initialized = false;
+            c->objcrop_valid = false;
+            return set_err(FPM_ERR_DEVICE,
+                           "split-mode handoff between the %d workgroups of a patch timed out; results are "
+                           "undefined, call fpm_init again", c->split_ks);
+        }
     }
     double led_ms = 0, crop_ms = 0;
     for (int it = 0; it < iters; ++it) {
@@ -700,7 +717,11 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
     info->support_px = c->support_px;
     info->device = c->device;
     info->device_bytes = c->bytes;
-    info->wg_per_patch = c->xch ? 2 : 1;
+    info->wg_per_patch = c->split_ks;
+    info->fused_kernel = c->path != FPM_PATH_FUSED ? FPM_KERNEL_GENERAL
+                         : c->fused_small      ? FPM_KERNEL_FUSED_SMALL
+                         : c->fused_mr         ? FPM_KERNEL_FUSED_NP200
+                                               : FPM_KERNEL_FUSED_NP256;
     return FPM_OK;
 }
 

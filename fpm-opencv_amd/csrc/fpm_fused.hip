@@ -75,21 +75,24 @@ struct FusedArgs {
     int btx0, bty0, nbx, nbt;
     float rnbx;                 // 1 / nbx
     unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
-    // split mode (NT 512, B <= CUs / 2): two workgroups per patch, half h of the
-    // columns each (split_layout); handoffs through xch with device-scope flags
-    int split;
-    float2 *xch;                // [B][2 halves][2 LED parities][kXchHalf]: F partial | tail F partial
-    int *flags;                 // [B][2]: half h's F partials of LED it published (it + 1);
-                                // then the abort flag, then [B][2] XCC_ID + 1 of each half
-    int *abort_flag;            // a handoff timed out: every workgroup leaves
+    // split mode (NT 512, KS = 2 or 4 workgroups per patch, KS * B <= CUs):
+    // workgroup p owns column part p (256 / KS columns); handoffs through xch
+    // with device-scope flags
+    float2 *xch;                // [B][KS parts][2 LED parities][kXchHalf]: F partial | tail F partial
+    int *flags;                 // [B][KS]: part p's F partials of LED it published (it + 1);
+                                // then the abort flag, then [B][KS] XCC_ID + 1 of each part
+    int *abort_flag;            // a handoff timed out: every workgroup leaves.  Sticky: the
+                                // per-launch reset does not clear it, fpm_run reports it
+    int stall_led;              // FPM_DEBUG_SPLIT_STALL (tests only): the last part stops
+                                // publishing from this LED on, forcing the timeout path; -1 off
 };
 
-// split-mode exchange area per patch (float2): each half's F partials of the
+// split-mode exchange area per patch (float2): each part's F partials of the
 // 512 lanes (12 slots each, lane-major) and of the <= 64 tail pixels, double
-// buffered by LED parity (a half overwrites its LED-i buffer only at LED i+2,
-// after the partner has published LED i+1, i.e. has read LED i's partials)
+// buffered by LED parity (a part overwrites its LED-i buffer only at LED i+2,
+// after every partner has published LED i+1, i.e. has read LED i's partials)
 constexpr int kXchTF = 12 * 512, kXchHalf = kXchTF + 64;
-constexpr int kXchPatch = 4 * kXchHalf;
+constexpr int xch_patch_elems(int ks) { return 2 * ks * kXchHalf; }
 
 // Handoff between the two workgroups of a patch (split mode).  Everything the
 // partner reads -- the exchange area, the updated spectrum window, the flags --
@@ -130,24 +133,31 @@ __device__ __forceinline__ void handoff_publish(int *flag, int value, bool local
         else __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-__device__ __forceinline__ bool handoff_wait(int *flag, int value, int *abort_flag, int *okslot, bool local,
-                                             __amdgpu_buffer_rsrc_t rflag, int flag_off) {
+// wait until every other part's flag (flags[0..KS), part `me` excluded) has
+// reached `value`
+template <int KS>
+__device__ __forceinline__ bool handoff_wait(int *flags, int me, int value, int *abort_flag, int *okslot, bool local,
+                                             __amdgpu_buffer_rsrc_t rflag) {
     if (threadIdx.x == 0) {
         int ok = 1;
-        for (int spins = 0;
-             (local ? ld_l2_i32(rflag, flag_off) : __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
-             value;
-             ++spins) {
-            if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                ok = 0;
-                break;
+#pragma unroll
+        for (int p = 0; p < KS; ++p) {
+            if (p == me || !ok) continue;
+            for (int spins = 0;
+                 (local ? ld_l2_i32(rflag, p * (int)sizeof(int))
+                        : __hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < value;
+                 ++spins) {
+                if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = 0;
+                    break;
+                }
+                if (spins > (1 << 23)) {
+                    __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
             }
-            if (spins > (1 << 23)) {
-                __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
         }
         *okslot = ok;
     }
@@ -165,10 +175,13 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
 
 __device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
 
-// half-row intermediate in LDS: row pitch 129 complex, so the 16 lanes of a
-// column read hit 16 different bank pairs
-constexpr int TH = fz::NP / 2;
-constexpr int TLD = TH + 1;
+// Column parts: T (the row IDFTs of the box rows) is held in LDS one column
+// part at a time -- two halves of 128 columns walked in turn by the
+// one-workgroup kernel (KS = 1), or the one part a split-mode workgroup owns
+// (KS = 2: a half, KS = 4: a quarter of 64 columns).  Row pitch part + 1
+// complex, so the 16 lanes of a column read hit 16 different bank pairs.
+constexpr int n_parts(int ks) { return ks == 1 ? 2 : ks; }
+constexpr int part_cols(int ks) { return fz::NP / n_parts(ks); }
 
 // Kernel configurations:
 //   NT = 512  : 32 groups, 2 FFT rows each, 2 waves per SIMD (256 VGPRs), full
@@ -188,16 +201,41 @@ struct FzCfg {
     static constexpr int XT = HALF ? 8 * XP : XTILE;  // exchange tile per group (complex)
 };
 
-template <int NT, bool SPLIT>
+// store the column part h of a row IDFT (r[m] = x[t + 16 m]) into the part's
+// T row: row[16 m'] = r[h MPP + m'] (h is block-uniform; one unrolled branch
+// per part keeps every register index static)
+// pruned forward row DFT of column part h (input row[16 m'] = x[t + 16 (h MPP + m')])
+template <bool HALF, int NPARTS, class TW, int HH = 0>
+__device__ __forceinline__ void row_dft_part(const float2 *row, float2 (&v)[16], float2 (&o)[6], float2 *scr,
+                                             const TW &wt, int t, int xrd, int h) {
+    constexpr int MPP = 16 / NPARTS;
+    if constexpr (HH < NPARTS) {
+        if (HH == h) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int m = 0; m < MPP; ++m) v[HH * MPP + m] = row[16 * m];
+            dft256_inpart_out6<HALF, NPARTS, HH>(v, o, scr, wt, t, xrd);
+        } else {
+            row_dft_part<HALF, NPARTS, TW, HH + 1>(row, v, o, scr, wt, t, xrd, h);
+        }
+    }
+}
+
+// KS workgroups per patch: 1 (both column halves in turn), or split mode with
+// 2 / 4 workgroups each owning one column part
+template <int NT, int KS>
 __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     using namespace fz;
     using C = FzCfg<NT>;
     constexpr int NG = C::NG, RPG = C::RPG, NW = C::NW;
     constexpr bool HALF = C::HALF, PARK = C::PARK;
+    static_assert(KS == 1 || (!PARK && (KS == 2 || KS == 4)), "split mode is NT 512 only");
+    constexpr int NPARTS = n_parts(KS), TH = part_cols(KS), TLD = TH + 1;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
     float2 *scr_all = sm;                           // NG * XT: per-group exchange tiles
-    float2 *th = scr_all + NG * C::XT;              // (nrows + 2) * TLD: half of T = row IDFTs of the box rows
+    float2 *th = scr_all + NG * C::XT;              // (nrows + 2) * TLD: one column part of T = row IDFTs of the box rows
     float2 *tw2 = th + (nrows + 2) * TLD;           // [m][t] = W256^{m t}  (after the zero + dummy rows)
     float2 *tw = tw2 + 256;                         // W256^k
     float2 *tailX = tw + 256;                       // MAXTAIL
@@ -215,17 +253,17 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     // exchange read base (see exchange16 / xchg)
     const int xrd = HALF ? opaque_int((t & 7) * XP) : exch_rbase(t);
     const int lane = tid & 63, w = tid >> 6;
-    // split mode: block k -> patch 8 (k / 16) + k % 8, half (k / 8) % 2, so the two
-    // halves of a patch are 8 blocks apart (the same XCD under round-robin
+    // split mode: block k -> patch 8 (k / (8 KS)) + k % 8, part (k / 8) % KS, so
+    // the parts of a patch are 8 blocks apart (the same XCD under round-robin
     // dispatch; only a speed matter, the handoff does not assume it)
-    constexpr bool split = SPLIT && !PARK;  // a separate instance: the one-workgroup kernel carries no split state
-    const int hown = split ? (int)((blockIdx.x >> 3) & 1) : -1;
-    const int b = split ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7)) : (int)blockIdx.x;
-    if (b >= st.B) return;  // split grid rounded up to 16 blocks (block-uniform)
-    const int hb = hown < 0 ? 0 : hown, he = hown < 0 ? 2 : hown + 1;  // halves this workgroup runs
-    float2 *xch = split ? a.xch + (size_t)b * kXchPatch : nullptr;
-    int *flg = split ? a.flags + 2 * b : nullptr;
-    int *xccs = split ? a.flags + 2 * st.B + 1 + 2 * b : nullptr;  // [2]: XCC_ID + 1 of each half
+    constexpr bool split = KS > 1;  // separate instances: the one-workgroup kernel carries no split state
+    const int hown = split ? (int)((blockIdx.x >> 3) % KS) : -1;
+    const int b = split ? (int)((blockIdx.x / (8 * KS)) * 8 + (blockIdx.x & 7)) : (int)blockIdx.x;
+    if (b >= st.B) return;  // split grid rounded up to 8 KS blocks (block-uniform)
+    const int hb = hown < 0 ? 0 : hown, he = hown < 0 ? NPARTS : hown + 1;  // parts this workgroup runs
+    float2 *xch = split ? a.xch + (size_t)b * xch_patch_elems(KS) : nullptr;
+    int *flg = split ? a.flags + KS * b : nullptr;
+    int *xccs = split ? a.flags + KS * st.B + 1 + KS * b : nullptr;  // [KS]: XCC_ID + 1 of each part
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * C::XT;
     const int nwords = (a.nbt + 31) >> 5;
@@ -327,22 +365,34 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     // handoffs, see ld_l2) -- one coherent exchange per launch
     bool local = false;
     // (descriptors are built unconditionally: the type has no empty state)
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(xch, 0, split ? kXchPatch * (int)sizeof(float2) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, split ? 2 * (int)sizeof(int) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc(xch, 0, split ? xch_patch_elems(KS) * (int)sizeof(float2) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, split ? KS * (int)sizeof(int) : 0, 0x00020000);
+    // the spectrum window of split mode (see sst): patch-sized descriptor
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(split ? st.spec + (size_t)b * L * L : nullptr, 0,
+                                          split ? L * L * (int)sizeof(float2) : 0, 0x00020000);
     if (split) {
         if (tid == 0) {
             const int mine = xcc_id() + 1;
             __hip_atomic_store(xccs + hown, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int other = 0;
-            for (int spins = 0; (other = __hip_atomic_load(xccs + 1 - hown, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)) == 0; ++spins) {
-                if (spins > (1 << 23) || __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
+            bool same = true;
+#pragma unroll
+            for (int p = 0; p < KS; ++p) {
+                if (p == hown) continue;
+                int other = 0;
+                for (int spins = 0; (other = __hip_atomic_load(xccs + p, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)) == 0; ++spins) {
+                    if (spins > (1 << 23) ||
+                        __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                __builtin_amdgcn_s_sleep(2);
+                same = same && other == mine;
             }
-            ccnt[1] = other == mine;
+            ccnt[1] = same;
         }
         __syncthreads();
         local = ccnt[1] != 0;
@@ -369,10 +419,22 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                           : __builtin_amdgcn_raw_buffer_load_b64(rx, lane_off, slot * (int)sizeof(float2),
                                                                  (int)(16u | (1u << 31))));
     };
-    // spectrum stores: in split mode both halves run the identical update and
-    // write identical values, and each reads back only its own writes (the
-    // next window, the dirty-tile re-scan), so plain stores serve both
-    auto sst = [&](float2 *p, float2 v) { *p = v; };
+    // spectrum stores: in split mode every part runs the identical update and
+    // writes identical values, and each reads back only its own writes (the
+    // next window, the dirty-tile re-scan).  Parts that share an XCD share its
+    // L2, so plain stores serve them.  Parts on different XCDs store with the
+    // device-scope (sc1) policy: a dirty line a lagging partner left in ITS
+    // L2 could otherwise be written back over this part's newer value after
+    // this part's own line was evicted, and a later miss would read it stale;
+    // sc1 stores reach memory before the flag that orders the next LED.
+    auto sst = [&](float2 *p, float2 v) {
+        if (split && !local) {
+            const int off = (int)((p - (st.spec + (size_t)b * L * L)) * (int)sizeof(float2));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs, off, 0, 16);
+        } else {
+            *p = v;
+        }
+    };
     const float epsn = st.eps * (float)(NP * NP);  // eps on the unscaled IDFT
     const float epsn_im = st.eps_im * (float)(NP * NP);
     __syncthreads();
@@ -468,20 +530,40 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = X[j][s];
                 idft256_in6<HALF>(v, r, scr, wt, t, xrd);
+                // keep the column part h: row[16 m'] = r[h MPP + m'] (one branch
+                // per part keeps every register index static; a shared helper
+                // made the compiler select between addresses of r and put r
+                // in scratch)
                 float2 *row = th + (g + NG * j) * TLD + t;
-                if (h == 0) {
+                if constexpr (NPARTS == 2) {
+                    if (h == 0) {
 #pragma unroll
-                    for (int m = 0; m < 8; ++m) row[16 * m] = r[m];
+                        for (int m = 0; m < 8; ++m) row[16 * m] = r[m];
+                    } else {
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) row[16 * m] = r[8 + m];
+                    }
                 } else {
+                    if (h == 0) {
 #pragma unroll
-                    for (int m = 0; m < 8; ++m) row[16 * m] = r[8 + m];
+                        for (int m = 0; m < 4; ++m) row[16 * m] = r[m];
+                    } else if (h == 1) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) row[16 * m] = r[4 + m];
+                    } else if (h == 2) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) row[16 * m] = r[8 + m];
+                    } else {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) row[16 * m] = r[12 + m];
+                    }
                 }
             }
             FPM_STAMP(7)
             // tail rows: direct sums, on the first half of the waves only (the
             // VALU arbiter favours them, so they finish their rows first)
             for (int idx = tid; tid < NT / 2 && idx < a.n_tail_rows * TH; idx += NT / 2) {
-                // q is wave-uniform (TH = 2 waves): the row's pixel range comes
+                // q is wave-uniform (TH = 1 or 2 waves): the row's pixel range comes
                 // from scalar loads; kx runs over a contiguous range, so the
                 // twiddle index advances by x per term
                 const int q = idx / TH, xl = idx - q * TH, x = xl + TH * h;
@@ -593,24 +675,10 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     for (int s = 0; s < 6; ++s) F[j][s] = make_float2(0.f, 0.f);
                     continue;
                 }
-                const float2 *row = th + (g + NG * j) * TLD + t;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
                 float2 o[6];
-                if (h == 0) {
+                row_dft_part<HALF, NPARTS>(th + (g + NG * j) * TLD + t, v, o, scr, wt, t, xrd, h);
 #pragma unroll
-                    for (int m = 0; m < 8; ++m) v[m] = row[16 * m];
-                    dft256_inhalf_out6<HALF, 0>(v, o, scr, wt, t, xrd);
-#pragma unroll
-                    for (int s = 0; s < 6; ++s) F[j][s] = o[s];
-                } else {
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) v[8 + m] = row[16 * m];
-                    dft256_inhalf_out6<HALF, 1>(v, o, scr, wt, t, xrd);
-#pragma unroll
-                    for (int s = 0; s < 6; ++s)
-                        F[j][s] = h == hb ? o[s] : cadd(PARK ? parkF(j, s) : F[j][s], o[s]);
-                }
+                for (int s = 0; s < 6; ++s) F[j][s] = h == hb ? o[s] : cadd(PARK ? parkF(j, s) : F[j][s], o[s]);
             }
             if (PARK && h == 0) {  // F is not held through the second half's passes A and B
 #pragma unroll
@@ -619,7 +687,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     for (int s = 0; s < 6; ++s) parkF(j, s) = F[j][s];
             }
             FPM_STAMP(8)
-            // tail pixels: 16 lanes sum 128 terms; first half of the waves only
+            // tail pixels: 16 lanes sum the part's TH terms; first half of the waves only
             for (int pp = g; g < NG / 2 && pp < a.n_tail_px; pp += NG / 2) {
                 const int2 px = tpx[pp];
                 const float2 *row = th + sig[px.x + KYOFF] * TLD;
@@ -629,9 +697,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 pf2 wk = pin(tw[((t + TH * h) * (px.y + NP)) & (NP - 1)]);
                 const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
 #pragma unroll
-                for (int m = 0; m < 8; ++m) {
+                for (int m = 0; m < TH / 16; ++m) {
                     s2p += pmul(pin(row[t + 16 * m]), wk);
-                    if (m < 7) wk = pmul(wk, wstep);
+                    if (m < TH / 16 - 1) wk = pmul(wk, wstep);
                 }
                 float2 s2 = pout(s2p);
 #pragma unroll
@@ -645,21 +713,24 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             FPM_STAMP(3)
         }
         if (split) {
-            // symmetric handoff: publish this half's F partials, take the
-            // partner's, and both halves run the same update (bit-identical:
-            // the sum is F_0 + F_1 in both, cadd commutes exactly); one handoff
-            // per LED, and no half waits for the other's update
+            // symmetric handoff: publish this part's F partials, take the
+            // partners', and every part runs the same update (bit-identical
+            // across the parts: each sums ((F_0 + F_1) + F_2) + F_3 in part
+            // order, its own partial from registers); one handoff per LED, and
+            // no part waits for another's update.  KS = 2 matches the
+            // one-workgroup kernel bit for bit (it forms F_0 + F_1 the same way).
             const int par = it & 1;
-            const int mine = (hown * 2 + par) * kXchHalf, other = ((1 - hown) * 2 + par) * kXchHalf;
+            const int mine = (hown * 2 + par) * kXchHalf;
+            if (it < a.stall_led || a.stall_led < 0 || hown != KS - 1) {
 #pragma unroll
-            for (int j = 0; j < RPG; ++j)
+                for (int j = 0; j < RPG; ++j)
 #pragma unroll
-                for (int s = 0; s < 6; ++s) xst(mine + (j * 6 + s) * NT, F[j][s]);
-            if (tid < a.n_tail_px) xst(mine + kXchTF, tailF[tid]);
-            FPM_STAMP(11)
-            handoff_publish(flg + hown, it + 1, local);
-            if (!handoff_wait(flg + 1 - hown, it + 1, a.abort_flag, ccnt + 1, local, rf,
-                              (1 - hown) * (int)sizeof(int))) {
+                    for (int s = 0; s < 6; ++s) xst(mine + (j * 6 + s) * NT, F[j][s]);
+                if (tid < a.n_tail_px) xst(mine + kXchTF, tailF[tid]);
+                FPM_STAMP(11)
+                handoff_publish(flg + hown, it + 1, local);
+            }
+            if (!handoff_wait<KS>(flg, hown, it + 1, a.abort_flag, ccnt + 1, local, rf)) {
                 aborted = true;
                 break;
             }
@@ -668,12 +739,26 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
                 for (int s = 0; s < 6; ++s) {
-                    const float2 o = xld(other + (j * 6 + s) * NT);
-                    F[j][s] = hown == 0 ? cadd(F[j][s], o) : cadd(o, F[j][s]);
+                    // F only matters on the support (KS = 2 keeps the
+                    // unmasked loads of the tuned two-part kernel)
+                    const bool in = KS == 2 || ((inmask[j] >> s) & 1);
+                    float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int p = 0; p < KS; ++p) {
+                        float2 o = F[j][s];
+                        if (p != hown) o = in ? xld(((p * 2 + par) * kXchHalf) + (j * 6 + s) * NT) : make_float2(0.f, 0.f);
+                        acc = p == 0 ? o : cadd(acc, o);
+                    }
+                    F[j][s] = acc;
                 }
             if (tid < a.n_tail_px) {
-                const float2 o = xld(other + kXchTF);
-                tailF[tid] = hown == 0 ? cadd(tailF[tid], o) : cadd(o, tailF[tid]);
+                float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int p = 0; p < KS; ++p) {
+                    const float2 o = p == hown ? tailF[tid] : xld(((p * 2 + par) * kXchHalf) + kXchTF);
+                    acc = p == 0 ? o : cadd(acc, o);
+                }
+                tailF[tid] = acc;
             }
         }
 
@@ -817,10 +902,10 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     __syncthreads();  // the last LED's red[32..]
     if (pupil_done) pm = pm_of_red();
     // stamps of the first and the last wave (the barrier waits show who is slow)
-    // (split mode: the first wave of each half's workgroup)
-    if (a.dbg && (split ? tid == 0 : (tid == 0 || tid == NT - 64)))
+    // (split mode: the first wave of the first and of the last part's workgroup)
+    if (a.dbg && (split ? (tid == 0 && (hown == 0 || hown == KS - 1)) : (tid == 0 || tid == NT - 64)))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[((split ? hown : tid) ? kStamps : 0) + i], acc[i]);
-    if (hown == 1) return;  // the first half's workgroup owns the per-patch state
+    if (hown > 0) return;  // the first part's workgroup owns the per-patch state
 
     // ---- write back the per-patch state
     loadP();
@@ -870,9 +955,10 @@ FusedGeom fused_geometry(int np, int r) {
     return g;
 }
 
-size_t fused_lds_bytes(int nt, int nbt, int n_tail_rows) {
+size_t fused_lds_bytes(int nt, int ks, int nbt, int n_tail_rows) {
     const int ng = nt / 16, xt = nt > 512 ? 8 * XP : XTILE;
-    return (size_t)(ng * xt + (fz::NROWS + n_tail_rows + 2) * TLD + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
+    const int tld = part_cols(ks) + 1;
+    return (size_t)(ng * xt + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
            (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
@@ -903,8 +989,8 @@ int fused_threads(int np, int r, int L, const DevState &st) {
     if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1) return 0;
     const Band bd = band_of(st);
     const char *e = getenv("FPM_FUSED_NT");
-    if (e && atoi(e) == 1024 && fused_lds_bytes(1024, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 1024;
-    if (fused_lds_bytes(512, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 512;
+    if (e && atoi(e) == 1024 && fused_lds_bytes(1024, 1, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 1024;
+    if (fused_lds_bytes(512, 1, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 512;
     return 0;
 }
 
@@ -913,24 +999,35 @@ size_t fused_park_elems(int nt, int B) { return nt > 512 ? (size_t)B * 2 * 6 * (
 
 size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
-// split mode (two workgroups per patch): exchange-area elements for B patches
-size_t fused_xch_elems(int B) { return (size_t)B * kXchPatch; }
+// split mode: exchange-area elements and flag words for B patches on KS parts
+size_t fused_xch_elems(int B, int ks) { return (size_t)B * xch_patch_elems(ks); }
+size_t fused_flag_words(int B, int ks) { return 2 * (size_t)ks * B + 1; }
 
-// Split mode pays off when one workgroup per patch would leave at least half
-// of the CUs idle (BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU)
-// and needs every block co-resident (the halves wait on each other), which the
-// cooperative launch guarantees or refuses.  FPM_NO_SPLIT=1 disables it.
-bool fused_split_wanted(int nt, int B, int n_cu) {
-    if (nt != 512 || B < 1 || getenv("FPM_NO_SPLIT")) return false;
-    return 16 * ((B + 7) / 8) <= n_cu;
+// Workgroups per patch of the Np 256 fused kernel (split mode, section 4.1b of
+// DESIGN.md).  Splitting pays off when one workgroup per patch would leave
+// CUs idle (BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU; a
+// 256-patch field strong-scaled over 4 / 8 GPUs: 64 / 32 per GPU) and needs
+// every block co-resident (the parts wait on each other), which the
+// cooperative launch guarantees or refuses: KS = 4 when 4 B <= CUs, KS = 2
+// when 2 B <= CUs, else 1.  FPM_NO_SPLIT=1 disables it; FPM_SPLIT=1/2/4 forces
+// a part count where the grid still fits.
+int fused_split_parts(int nt, int B, int n_cu) {
+    if (nt != 512 || B < 1 || getenv("FPM_NO_SPLIT")) return 1;
+    auto fits = [&](int ks) { return 8 * ks * ((B + 7) / 8) <= n_cu; };
+    if (const char *e = getenv("FPM_SPLIT")) {
+        const int ks = atoi(e);
+        return (ks == 2 || ks == 4) && fits(ks) ? ks : 1;
+    }
+    return fits(4) ? 4 : fits(2) ? 2 : 1;
 }
 
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  float2 *pscr, int nt, unsigned long long *dbg, float2 *xch, int *flags,
+                                  float2 *pscr, int nt, int ks, unsigned long long *dbg, float2 *xch, int *flags,
                                   hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
     if (!g.ok || (nt != 512 && nt != 1024)) return hipErrorInvalidValue;
+    if (ks != 1 && (nt != 512 || (ks != 2 && ks != 4) || !xch || !flags)) return hipErrorInvalidValue;
     if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
         return hipErrorInvalidValue;
     FusedArgs a;
@@ -966,29 +1063,36 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.nbt = bd.nbt;
     a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
-    a.split = xch != nullptr;
-    a.xch = xch;
-    a.flags = flags;
-    a.abort_flag = flags ? flags + 2 * st.B : nullptr;
-    const size_t lds = fused_lds_bytes(nt, a.nbt, g.n_tail_rows);
+    a.xch = ks > 1 ? xch : nullptr;
+    a.flags = ks > 1 ? flags : nullptr;
+    a.abort_flag = ks > 1 ? flags + ks * st.B : nullptr;
+    {
+        const char *e = getenv("FPM_DEBUG_SPLIT_STALL");
+        a.stall_led = e ? atoi(e) : -1;
+    }
+    const size_t lds = fused_lds_bytes(nt, ks, a.nbt, g.n_tail_rows);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024, false>
-                     : a.split  ? (const void *)k_fused_iteration<512, true>
-                                : (const void *)k_fused_iteration<512, false>;
+    const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024, 1>
+                     : ks == 4  ? (const void *)k_fused_iteration<512, 4>
+                     : ks == 2  ? (const void *)k_fused_iteration<512, 2>
+                                : (const void *)k_fused_iteration<512, 1>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    if (a.split) {
-        if (nt != 512) return hipErrorInvalidValue;
-        // flags count LEDs of this launch: start from zero (and no abort)
-        e = hipMemsetAsync(flags, 0, (4 * (size_t)st.B + 1) * sizeof(int), s);
+    if (ks > 1) {
+        // flags count LEDs of this launch and XCC ids are re-learnt: both start
+        // from zero; the abort word between them is sticky (fpm_run reads and
+        // clears it, so a timeout in any iteration of a multi-iteration run
+        // is reported, and every later launch leaves at once)
+        e = hipMemsetAsync(flags, 0, (size_t)ks * st.B * sizeof(int), s);
+        if (e == hipSuccess) e = hipMemsetAsync(flags + ks * st.B + 1, 0, (size_t)ks * st.B * sizeof(int), s);
         if (e != hipSuccess) return e;
         void *args[] = {&a};
-        return hipLaunchCooperativeKernel(fn, dim3(16 * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
+        return hipLaunchCooperativeKernel(fn, dim3(8 * ks * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
     }
     if (nt == 1024)
-        hipLaunchKernelGGL((k_fused_iteration<1024, false>), dim3(st.B), dim3(1024), lds, s, a);
+        hipLaunchKernelGGL((k_fused_iteration<1024, 1>), dim3(st.B), dim3(1024), lds, s, a);
     else
-        hipLaunchKernelGGL((k_fused_iteration<512, false>), dim3(st.B), dim3(512), lds, s, a);
+        hipLaunchKernelGGL((k_fused_iteration<512, 1>), dim3(st.B), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 

@@ -95,6 +95,31 @@ __device__ __forceinline__ void pdft16_inhalf(pf2 (&v)[16], pf2 (&r)[16]) {
     for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
 }
 
+// 16-point DFT whose input is zero outside v[4Q .. 4Q+3] (one quarter of a
+// row, split mode with four workgroups per patch): the first radix-4 stage
+// sees one non-zero input per butterfly, a -> (a, W4^Q a, W4^2Q a, W4^3Q a)
+template <bool INV, int Q>
+__device__ __forceinline__ void pdft16_inquarter(pf2 (&v)[16], pf2 (&r)[16]) {
+    const pf2 z = {0.f, 0.f};
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        const pf2 a = v[k1 + 4 * Q];
+        if constexpr (Q == 0) {
+            v[k1] = a; v[k1 + 4] = a; v[k1 + 8] = a; v[k1 + 12] = a;
+        } else if constexpr (Q == 1) {   // pbf4 of (0, a, 0, 0)
+            v[k1] = a; v[k1 + 4] = padd_w4<INV>(z, a); v[k1 + 8] = -a; v[k1 + 12] = psub_w4<INV>(z, a);
+        } else if constexpr (Q == 2) {   // (0, 0, a, 0)
+            v[k1] = a; v[k1 + 4] = -a; v[k1 + 8] = a; v[k1 + 12] = -a;
+        } else {                         // (0, 0, 0, a)
+            v[k1] = a; v[k1 + 4] = psub_w4<INV>(z, a); v[k1 + 8] = -a; v[k1 + 12] = padd_w4<INV>(z, a);
+        }
+    }
+    pmid_tw<INV>(v);
+    pstage2<INV>(v);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
+}
+
 // Exchange of the four-step transforms.  NT = 512: the full 16 x 16 tile per
 // group (dft16.hpp exchange16).  NT = 1024: 64 groups' full tiles (147 KB)
 // do not fit beside the half-T, so each group owns HALF a tile (8 rows, 73.7 KB
@@ -205,6 +230,29 @@ __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[
     to_pk(v, pv);
     pdft16_out6<false>(pv, po);
     from_pk(po, o);
+}
+
+// forward 256-point DFT of part P of NPARTS (x = t + 16 n2, n2 in
+// [P 16/NPARTS, (P+1) 16/NPARTS), zero elsewhere), output o[s] = X[t + 16 SK[s]]
+template <bool HALF, int NPARTS, int P, class TW>
+__device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt,
+                                                   int t, int xrd) {
+    if constexpr (NPARTS == 2) {
+        dft256_inhalf_out6<HALF, P>(v, o, scr, wt, t, xrd);
+    } else {
+        static_assert(NPARTS == 4, "two or four column parts");
+        pf2 pv[16], py[16], po[6];
+        to_pk(v, pv);
+        pdft16_inquarter<false, P>(pv, py);
+#pragma unroll
+        for (int k1 = 1; k1 < 16; ++k1) py[k1] = pmul(py[k1], pin(wt[k1]));
+        float2 y[16];
+        from_pk(py, y);
+        xchg<HALF>(scr, t, xrd, y, v);
+        to_pk(v, pv);
+        pdft16_out6<false>(pv, po);
+        from_pk(po, o);
+    }
 }
 
 }  // namespace fpm

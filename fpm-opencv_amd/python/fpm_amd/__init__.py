@@ -35,6 +35,11 @@ FLAG_OBJCROP_LAST_ONLY = 1
 FLAG_SPEC_FP16 = 2          # fp16 spectrum storage, fp32 arithmetic (config 5)
 FLAG_SCALAR_RE_ONLY = 4     # legacy: cv::add(UMat c2, double) on the real channel only (fpm_hip.h)
 
+# fpm_info.fused_kernel: the LED-update kernel of the context (fpm_hip.h FPM_KERNEL_*)
+KERNEL_GENERAL, KERNEL_FUSED_NP256, KERNEL_FUSED_NP200, KERNEL_FUSED_SMALL = 0, 1, 2, 3
+KERNEL_NAMES = {KERNEL_GENERAL: "general_led_step", KERNEL_FUSED_NP256: "k_fused_iteration",
+                KERNEL_FUSED_NP200: "k_fused_mr", KERNEL_FUSED_SMALL: "k_fused_small"}
+
 # every symbol include/fpm_hip.h declares
 HIP_SYMBOLS = (
     "fpm_create", "fpm_destroy", "fpm_upload_stack", "fpm_upload_stack_device",
@@ -74,7 +79,8 @@ class fpm_frames(C.Structure):
 
 class fpm_info(C.Structure):
     _fields_ = [("path", C.c_int32), ("box", C.c_int32), ("support_px", C.c_int32),
-                ("device", C.c_int32), ("device_bytes", C.c_size_t), ("wg_per_patch", C.c_int32)]
+                ("device", C.c_int32), ("device_bytes", C.c_size_t), ("wg_per_patch", C.c_int32),
+                ("fused_kernel", C.c_int32)]
 
 
 class fpm_timing(C.Structure):

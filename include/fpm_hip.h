@@ -115,6 +115,12 @@ typedef struct fpm_problem {
 
 typedef struct fpm_ctx fpm_ctx;
 
+/* fpm_info.fused_kernel: the LED-update kernel fpm_run launches */
+#define FPM_KERNEL_GENERAL      0  /* general path: 4-5 launches per LED          */
+#define FPM_KERNEL_FUSED_NP256  1  /* k_fused_iteration (Np 256, r <= 34)          */
+#define FPM_KERNEL_FUSED_NP200  2  /* k_fused_mr (Np 200)                          */
+#define FPM_KERNEL_FUSED_SMALL  3  /* k_fused_small (Np <= 96)                     */
+
 /* Which path the context runs and its per-launch geometry. */
 typedef struct fpm_info {
     int32_t path;          /* FPM_PATH_GENERAL or FPM_PATH_FUSED */
@@ -122,8 +128,9 @@ typedef struct fpm_info {
     int32_t support_px;    /* pixels in the pupil support disk                  */
     int32_t device;
     size_t  device_bytes;  /* device memory owned by the context               */
-    int32_t wg_per_patch;  /* fused Np 256 path: 2 when each patch is split over
-                              two workgroups (n_patch <= CUs / 2), else 1       */
+    int32_t wg_per_patch;  /* fused Np 256 path (split mode): 4 when 4*n_patch
+                              <= CUs, 2 when 2*n_patch <= CUs, else 1          */
+    int32_t fused_kernel;  /* FPM_KERNEL_*                                      */
 } fpm_info;
 
 /* Per-kernel timing of the most recent fpm_run, from HIP events recorded on

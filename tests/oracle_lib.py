@@ -50,18 +50,28 @@ def run_fpm(stack, order, x0, y0, np_, L, r, d1, d2, iters, eps=float(np.float32
 
 
 def run_fpm_batch(stack, order, x0, y0, np_, L, r, d1, d2, iters, threads, outputs=True,
-                  eps=float(np.float32(1e-10)), all_channels=True):
-    """stack uint16 [n_stack][B][Np][Np]; B patches on `threads` threads."""
+                  eps=float(np.float32(1e-10)), all_channels=True, pupil=False, objF=False):
+    """stack uint16 [n_stack][B][Np][Np]; B patches on `threads` threads.
+    Returns objCrop [B][L][L] (None when outputs=False), or with pupil=True
+    (objF=True) a dict of objCrop and pupil [B][Np][Np] (centred, like
+    run_fpm) (and objF [B][L][L])."""
     lib = load()
     st = np.ascontiguousarray(stack, np.uint16)
     B = st.shape[1]
     order, x0, y0 = (np.ascontiguousarray(v, np.int32) for v in (order, x0, y0))
     dp = C.POINTER(C.c_double)
     objCrop = np.zeros((B, L, L), np.complex128) if outputs else None
+    pupil = pupil or objF
+    pup = np.zeros((B, np_, np_), np.complex128) if (outputs and pupil) else None
+    oF = np.zeros((B, L, L), np.complex128) if (outputs and objF) else None
     rc = lib.oracle_run_fpm_batch(np_, L, len(x0), B, st.ctypes.data_as(C.POINTER(C.c_uint16)), len(order),
-                                  _ip(order), _ip(x0), _ip(y0), r, d1, d2, eps, iters, int(all_channels), threads, None,
-                                  objCrop.ctypes.data_as(dp) if outputs else None, None)
+                                  _ip(order), _ip(x0), _ip(y0), r, d1, d2, eps, iters, int(all_channels), threads,
+                                  oF.ctypes.data_as(dp) if oF is not None else None,
+                                  objCrop.ctypes.data_as(dp) if outputs else None,
+                                  pup.ctypes.data_as(dp) if pup is not None else None)
     assert rc == 0, rc
+    if pupil and outputs:
+        return dict(objCrop=objCrop, pupil=pup, **({"objF": oF} if objF else {}))
     return objCrop
 
 

@@ -72,9 +72,12 @@ def test_config2_mono_dome_64_patches_batched():
     assert np.isfinite(out["objCrop"]).all()
     sample = (0, 37, 63)
     refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 2,
-                                    threads=3)
+                                    threads=3, pupil=True)
     for i, b in enumerate(sample):
-        assert rel_l2(out["objCrop"][b], refs[i]) < 5e-5, b
+        for k in ("objCrop", "pupil"):
+            e = rel_l2(out[k][b], refs[k][i])
+            print(f"config2 patch {b} {k} rel L2 {e:.2e}")
+            assert e < 5e-5, (k, b, e)
 
 
 def _probe_geometry(name):
@@ -110,9 +113,12 @@ def test_config3_dogstomach_literal_256_patches():
     sample = (0, 128, 255)
     assert len({int(idx[b]) for b in sample}) == 3
     refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 2,
-                                    threads=3)
+                                    threads=3, pupil=True)
     for i, b in enumerate(sample):
-        assert rel_l2(out["objCrop"][b], refs[i]) < 5e-5, b
+        for k in ("objCrop", "pupil"):
+            e = rel_l2(out[k][b], refs[k][i])
+            print(f"config3 patch {b} {k} rel L2 {e:.2e}")
+            assert e < 5e-5, (k, b, e)
     # identical inputs give identical bits whatever the patch slot
     np.testing.assert_array_equal(out["objCrop"][0], out["objCrop"][7])
     np.testing.assert_array_equal(out["pupil"][128], out["pupil"][2])
@@ -136,9 +142,12 @@ def test_config4_single_gpu_shard_128_patches():
     sample = (0, 63, 127)
     assert len({int(idx[b]) for b in sample}) == 3
     refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 1,
-                                    threads=3)
+                                    threads=3, pupil=True)
     for i, b in enumerate(sample):
-        assert rel_l2(out["objCrop"][b], refs[i]) < 1e-5, b
+        for k in ("objCrop", "pupil"):
+            e = rel_l2(out[k][b], refs[k][i])
+            print(f"config4 patch {b} {k} rel L2 {e:.2e}")
+            assert e < 1e-5, (k, b, e)
 
 
 def test_config5_geometry_np1024_l4096():
@@ -202,10 +211,33 @@ def test_fp16_storage_rejected_on_fused_path():
     assert e.value.code == fpm_amd.FPM_ERR_INVAL
 
 
+def test_config5_fp16_storage_65_leds_2_iterations():
+    """Config 5 at scale: Np 1024, L 4096, naRadius 333, fp16 spectrum storage,
+    65 LEDs spread over the bench's whole 512-LED grid (every 8th LED of its
+    centre-out order plus the outermost one, so the outermost sub-apertures and
+    the spectrum edge are exercised), 2 iterations vs the fp64 oracle."""
+    import bench
+    import oracle_lib
+    geo = bench.config_geometry("c5")
+    Np, L, r = geo["np_"], geo["L"], geo["r"]
+    pick = list(range(0, geo["n_led"], 8)) + [geo["n_led"] - 1]
+    x0, y0 = np.asarray(geo["x0"])[pick], np.asarray(geo["y0"])[pick]
+    assert len(pick) == 65 and max(np.abs(x0 - (L // 2 - Np // 2)).max(), np.abs(y0 - (L // 2 - Np // 2)).max()) > 1000
+    order = np.arange(len(pick), dtype=np.int32)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=15)
+    ref = oracle_lib.run_fpm(stack[:, 0], order, x0, y0, Np, L, r, geo["d1"], geo["d2"], 2)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, geo["d1"], geo["d2"], n_patch=1, flags=fpm_amd.FLAG_SPEC_FP16)
+    out = fpm_amd.run_fpm(prob, stack, 2)
+    for k in ("objCrop", "objF", "pupil"):
+        e = rel_l2(out[k][0], ref[k])
+        print(f"config5 fp16 65 LEDs 2 it {k} rel L2 {e:.2e}")
+        assert e < FP16_TOL, (k, e)
+
+
 def test_config5_fp16_storage_np1024_l4096():
     """Config 5 as BASELINE.json names it: Np 1024, L 4096 spectrum held in
     fp16 (half the bytes of fp32 complex), fp32 arithmetic; 6 LEDs, 1
-    iteration vs the fp64 oracle."""
+    iteration vs the fp64 oracle, and the device-memory saving."""
     import oracle_lib
     from tools.synth import grid_geometry
     Np, L, r = 1024, 4096, 333

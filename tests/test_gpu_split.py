@@ -1,10 +1,17 @@
-"""Split mode of the Np 256 fused kernel (fpm_fused.hip): with n_patch <= CUs/2
-each patch runs on two workgroups (one column half each) that hand the row-DFT
-partials and the updated pupil to each other through device-scope flags
-(BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU).  The split path
-adds the two halves' partials in the same order as the one-workgroup path, so
-the two must agree bit for bit; parity with the oracle is covered by every
-small-batch fused test (tests/test_gpu_parity.py runs n_patch 2, i.e. split).
+"""Split mode of the Np 256 fused kernel (fpm_fused.hip): with
+KS * n_patch <= CUs each patch runs on KS = 2 or 4 workgroups (one column part
+each) that exchange their row-DFT partials once per LED through device-scope
+flags (BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU; the
+256-patch metric field strong-scaled over 4 / 8 GPUs = 64 / 32 per GPU).
+
+  * KS = 2 adds the two partials in the same order as the one-workgroup kernel
+    (F_0 + F_1), so the two agree bit for bit.
+  * KS = 4 sums four quarter partials ((F_0 + F_1) + F_2) + F_3: the same
+    arithmetic up to fp32 rounding (measured rel. L2 vs KS = 1 stated in the
+    assertion), deterministic run to run, and checked against the fp64 oracle.
+  * A handoff that times out (forced with FPM_DEBUG_SPLIT_STALL) fails fpm_run
+    even when it happens in an earlier iteration of a multi-iteration run, and
+    the context must be re-initialised.
 """
 import os
 
@@ -18,9 +25,10 @@ from tools.synth import grid_geometry, make_stack
 pytestmark = pytest.mark.gpu
 
 
-def _solve(prob, stack, iters, no_split):
-    if no_split:
-        os.environ["FPM_NO_SPLIT"] = "1"
+def _solve(prob, stack, iters, ks):
+    """ks: workgroups per patch to force (FPM_SPLIT / FPM_NO_SPLIT)."""
+    key = "FPM_NO_SPLIT" if ks == 1 else "FPM_SPLIT"
+    os.environ[key] = "1" if ks == 1 else str(ks)
     try:
         with fpm_amd.Solver(prob) as s:
             info = s.info()
@@ -29,36 +37,95 @@ def _solve(prob, stack, iters, no_split):
             s.run(iters)
             return info.wg_per_patch, s.download()
     finally:
-        os.environ.pop("FPM_NO_SPLIT", None)
+        os.environ.pop(key, None)
 
 
 @pytest.mark.parametrize("r,nside,step,B,iters", [(33, 5, 20, 5, 2), (34, 3, 30, 9, 1), (10, 4, 24, 1, 3)],
                          ids=["r33_B5_it2", "r34_B9_it1", "r10_B1_it3"])
-def test_split_equals_one_workgroup_per_patch(r, nside, step, B, iters):
+def test_split2_equals_one_workgroup_per_patch(r, nside, step, B, iters):
     Np, L = 256, 512
     x0, y0, order = grid_geometry(Np, L, nside, step)
     stack = make_stack(Np, L, r, x0, y0, n_patch=B, seed=5 + r)
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=B, path=fpm_amd.PATH_FUSED)
-    wg2, out2 = _solve(prob, stack, iters, no_split=False)
-    wg1, out1 = _solve(prob, stack, iters, no_split=True)
+    wg2, out2 = _solve(prob, stack, iters, 2)
+    wg1, out1 = _solve(prob, stack, iters, 1)
     assert (wg2, wg1) == (2, 1)
     for k in ("objF", "objCrop", "pupil"):
         np.testing.assert_array_equal(out2[k], out1[k], err_msg=k)
 
 
-def test_split_metric_geometry_many_handoffs():
-    """293 LEDs of the metric geometry (586 handoffs per iteration) on 3 patches:
-    split vs one workgroup per patch, and both finite and non-trivial."""
+@pytest.mark.parametrize("r,nside,step,B,iters", [(33, 5, 20, 5, 2), (34, 3, 30, 9, 1), (10, 4, 24, 1, 3)],
+                         ids=["r33_B5_it2", "r34_B9_it1", "r10_B1_it3"])
+def test_split4_matches_one_workgroup_and_oracle(r, nside, step, B, iters):
+    import oracle_lib
+    Np, L = 256, 512
+    x0, y0, order = grid_geometry(Np, L, nside, step)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=B, seed=7 + r)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=B, path=fpm_amd.PATH_FUSED)
+    wg4, out4 = _solve(prob, stack, iters, 4)
+    wg4b, out4b = _solve(prob, stack, iters, 4)
+    wg1, out1 = _solve(prob, stack, iters, 1)
+    assert (wg4, wg4b, wg1) == (4, 4, 1)
+    for k in ("objF", "objCrop", "pupil"):
+        np.testing.assert_array_equal(out4[k], out4b[k], err_msg=k)      # deterministic
+        for b in range(B):
+            e = rel_l2(out4[k][b], out1[k][b])
+            assert e < 2e-6, (k, b, e)                                     # fp32 summation order only
+    tol = 1e-5 if iters == 1 else 5e-5
+    for b in sorted({0, B - 1}):
+        ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, 10, 3, iters)
+        for k in ("objF", "objCrop", "pupil"):
+            assert rel_l2(out4[k][b], ref[k]) < tol, (k, b)
+
+
+@pytest.mark.parametrize("ks", [2, 4])
+def test_split_metric_geometry_many_handoffs(ks):
+    """293 LEDs of the metric geometry (one handoff per LED) on 3 patches:
+    split vs one workgroup per patch, both finite and non-trivial."""
     from test_gpu_configs import _probe_geometry, _tiled_stack
     p, x0, y0 = _probe_geometry("geometry_dogStomach_metric.json")
     Np, L, r = p["np"], p["nlarge"], p["na_radius"]
     order = np.arange(len(x0))
     stack, _ = _tiled_stack(Np, L, r, x0, y0, 3, 3, seed=11)
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=3, path=fpm_amd.PATH_FUSED)
-    wg2, out2 = _solve(prob, stack, 1, no_split=False)
-    wg1, out1 = _solve(prob, stack, 1, no_split=True)
-    assert (wg2, wg1) == (2, 1)
-    assert np.isfinite(out2["objCrop"]).all()
+    wgs, outs = _solve(prob, stack, 1, ks)
+    wg1, out1 = _solve(prob, stack, 1, 1)
+    assert (wgs, wg1) == (ks, 1)
+    assert np.isfinite(outs["objCrop"]).all()
     for k in ("objF", "objCrop", "pupil"):
-        np.testing.assert_array_equal(out2[k], out1[k], err_msg=k)
-    assert rel_l2(out2["objCrop"][0], out2["objCrop"][1]) > 1e-3  # patches differ
+        if ks == 2:
+            np.testing.assert_array_equal(outs[k], out1[k], err_msg=k)
+        else:
+            for b in range(3):
+                assert rel_l2(outs[k][b], out1[k][b]) < 2e-6, (k, b)
+    assert rel_l2(outs["objCrop"][0], outs["objCrop"][1]) > 1e-3  # patches differ
+
+
+def test_split_handoff_timeout_is_reported_and_sticky():
+    """The last part stops publishing at LED 3 of the first iteration: its
+    partners time out (~seconds), the abort word stays set through the second
+    launch of fpm_run(2), the run fails with FPM_ERR_DEVICE, and the context
+    needs fpm_init again (after which a clean run succeeds)."""
+    Np, L, r = 256, 512, 10
+    x0, y0, order = grid_geometry(Np, L, 3, 24)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=3)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=1, path=fpm_amd.PATH_FUSED)
+    with fpm_amd.Solver(prob) as s:
+        assert s.info().wg_per_patch == 4
+        s.upload(stack)
+        s.init()
+        os.environ["FPM_DEBUG_SPLIT_STALL"] = "3"
+        try:
+            with pytest.raises(fpm_amd.FpmError) as e:
+                s.run(2)
+        finally:
+            os.environ.pop("FPM_DEBUG_SPLIT_STALL", None)
+        assert e.value.code == fpm_amd.FPM_ERR_DEVICE
+        assert "timed out" in str(e.value)
+        with pytest.raises(fpm_amd.FpmError) as e2:  # state is undefined until re-initialised
+            s.run(1)
+        assert e2.value.code == fpm_amd.FPM_ERR_STATE
+        s.init()
+        s.run(1)
+        out = s.download()
+    assert np.isfinite(out["objCrop"]).all()

@@ -37,9 +37,18 @@ N_SIMD = 1024
 
 
 def short(name):
-    for k in ("k_fused_iteration", "k_fused_mr", "k_meas_layout", "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows",
+    """Kernel key: the Np 256 fused kernel keeps its template instance
+    (k_fused_iteration<NT,KS>: threads, workgroups per patch) so a profile of
+    the split-mode instance is never read as the one-workgroup kernel's."""
+    import re
+    m = re.search(r"k_fused_iteration<(\d+),\s*(\d+)>", name)
+    if m:
+        return f"k_fused_iteration<{m.group(1)},{m.group(2)}>"
+    for k in ("k_fused_mr", "k_fused_small", "k_meas_layout", "k_meas_transpose_tiles", "k_meas_transpose",
+              "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows600", "k_crop_cols600", "k_crop_rows",
               "k_crop_cols", "k_colpass_wave", "k_colpass_tiled", "k_gather_rowifft_tiled",
-              "k_rowfft_update_tiled", "k_tile_rows", "k_pupil_commit"):
+              "k_rowfft_update_tiled", "k_rows1024_inv", "k_rows1024_fwd", "k_cols1024", "k_tile_rows",
+              "k_tile_max_all", "k_row_max_all", "k_pupil_commit"):
         if k in name:
             return k
     return name.split("(")[0][:60]
@@ -80,7 +89,7 @@ def main():
                 k = short(r["Kernel_Name"])
                 v = float(r["Counter_Value"])
                 acc[k][r["Counter_Name"]].append(v)
-                if k == "k_meas_layout" and r["Counter_Name"] == "FETCH_SIZE":
+                if k == "k_meas_layout" and r["Counter_Name"] == "FETCH_SIZE" and "Grid_Size" in r:
                     perm.append((int(r["Grid_Size"]), v * 1024.0))
     raw = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
     res = {"src_hash": src_hash(), "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
