@@ -231,6 +231,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     constexpr int NG = C::NG, RPG = C::RPG, NW = C::NW;
     constexpr bool HALF = C::HALF, PARK = C::PARK;
     static_assert(KS == 1 || (!PARK && (KS == 2 || KS == 4)), "split mode is NT 512 only");
+    static_assert(6 * RPG * 16 <= C::XT, "pupil numerators are parked in the group's exchange tile");
     constexpr int NPARTS = n_parts(KS), TH = part_cols(KS), TLD = TH + 1;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
@@ -790,8 +791,10 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 float2 num;
                 float oa;
                 const float2 nv = slot_update(F[j][s], Opre[j][s], P[j][s], pm, st, num, oa);
-                // this group's own half-T row is no longer read: park the numerator there
-                th[(g + NG * j) * TLD + s * 16 + t] = num;
+                // park the numerator in this group's own exchange tile (idle
+                // until the next LED's pass A; 6 RPG 16 <= its 8 XP complex);
+                // a T row is too narrow for it when the part is 64 columns
+                scr[(j * 6 + s) * 16 + t] = num;
                 if ((inmask[j] >> s) & 1) {
                     sst(srow + (kyr[j] * L + t) + soff(s), nv);  // read by a split partner
                     note(yc + kyr[j], xc + kx, oa, cmag(nv));
@@ -876,7 +879,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         for (int j = 0; j < RPG; ++j)
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                const float2 n = th[(g + NG * j) * TLD + s * 16 + t];
+                const float2 n = scr[(j * 6 + s) * 16 + t];
                 P[j][s] = make_float2(P[j][s].x + n.x * rom, P[j][s].y + n.y * rom);
                 pmx = fmaxf(pmx, cabs2(P[j][s]));
                 if (PARK) parkP(j, s) = P[j][s];
@@ -888,7 +891,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         // red[32..47] is not used by the max phase, so no barrier is needed
         // before writing it; nothing read below is rewritten by another
         // thread before the next LED's first barrier (numerators sit in this
-        // thread's own half-T slots, tailX was last read in pass A).
+        // thread's own exchange-tile slots, tailX was last read in pass A).
         // max|P| is first needed by the next LED's object update, several
         // barriers later: it is reduced there (pm_of_red), not behind a
         // barrier of its own here.
