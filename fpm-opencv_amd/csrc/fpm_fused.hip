@@ -736,18 +736,32 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 break;
             }
             FPM_STAMP(12)
+            // every partner partial is loaded before the first is used (one
+            // L2 round trip for all of them); F only matters on the support
+            // (KS = 2 keeps the unmasked loads of the tuned two-part kernel)
+            float2 ox[KS > 1 ? KS - 1 : 1][RPG][6];
+#pragma unroll
+            for (int q = 0; q < KS - 1; ++q) {
+                const int pp = q < hown ? q : q + 1;  // partner part (block-uniform)
+                const int base = (pp * 2 + par) * kXchHalf;
+#pragma unroll
+                for (int j = 0; j < RPG; ++j)
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) {
+                        const bool in = KS == 2 || ((inmask[j] >> s) & 1);
+                        ox[q][j][s] = in ? xld(base + (j * 6 + s) * NT) : make_float2(0.f, 0.f);
+                    }
+            }
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
 #pragma unroll
                 for (int s = 0; s < 6; ++s) {
-                    // F only matters on the support (KS = 2 keeps the
-                    // unmasked loads of the tuned two-part kernel)
-                    const bool in = KS == 2 || ((inmask[j] >> s) & 1);
                     float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
                     for (int p = 0; p < KS; ++p) {
-                        float2 o = F[j][s];
-                        if (p != hown) o = in ? xld(((p * 2 + par) * kXchHalf) + (j * 6 + s) * NT) : make_float2(0.f, 0.f);
+                        // part p's partial: own registers, or partner slot p (p < hown) / p - 1
+                        const float2 lo = ox[p < KS - 1 ? p : KS - 2][j][s], hi = ox[p > 0 ? p - 1 : 0][j][s];
+                        const float2 o = p == hown ? F[j][s] : p < hown ? lo : hi;
                         acc = p == 0 ? o : cadd(acc, o);
                     }
                     F[j][s] = acc;
