@@ -153,6 +153,8 @@ def kernel_name(info):
     import fpm_amd
     if info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256:
         return f"k_fused_iteration<512,{info.wg_per_patch}>"
+    if info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256_DIST:
+        return f"k_fused_dist<{info.wg_per_patch}>"
     return fpm_amd.KERNEL_NAMES[info.fused_kernel]
 
 

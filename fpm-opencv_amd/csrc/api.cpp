@@ -53,6 +53,12 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
 size_t fused_xch_elems(int B, int ks);
 size_t fused_flag_words(int B, int ks);
 int fused_split_parts(int nt, int B, int n_cu);
+// distributed mode of the Np 256 kernel (fused_dist.hip)
+size_t fused_dist_elems(int B, int ks);
+int fused_dist_parts(int B, int n_cu, int r, int L);
+hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
+                             const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
+                             float2 *area, int *flags, hipStream_t s);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
@@ -128,7 +134,8 @@ struct fpm_ctx {
                                     // kernel and the Np 1024 general path, transposed); 0: C-ABI
     float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
     int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
-    int split_ks = 1;               // split mode: workgroups per patch (2 or 4), else 1
+    int split_ks = 1;               // split / distributed mode: workgroups per patch (2, 4, 8), else 1
+    bool dist = false;              // distributed mode (fused_dist.hip) instead of split mode
     float2 *xch = nullptr;          //   exchange area
     int *split_flags = nullptr;     //   handoff flags [KS B] + sticky abort flag + XCC ids [KS B]
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
@@ -362,9 +369,15 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         int n_cu = 0, coop = 0;
         (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
         (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device);
-        c->split_ks = (c->fused_nt && coop) ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
+        // small batches: every phase distributed over KS workgroups per patch
+        // (fused_dist.hip), else split mode (column parts only), else one
+        // workgroup per patch
+        const int dks = (c->fused_nt == 512 && coop) ? fused_dist_parts(B, n_cu, r, L) : 0;
+        c->dist = dks > 1;
+        c->split_ks = c->dist ? dks : (c->fused_nt && coop) ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
         if (c->split_ks > 1) {
-            if ((rc = dalloc(c, &c->xch, fused_xch_elems(B, c->split_ks)))) return fail(rc);
+            const size_t nx = c->dist ? fused_dist_elems(B, c->split_ks) : fused_xch_elems(B, c->split_ks);
+            if ((rc = dalloc(c, &c->xch, nx))) return fail(rc);
             const size_t nf = fused_flag_words(B, c->split_ks);
             if ((rc = dalloc(c, &c->split_flags, nf))) return fail(rc);
             if (hipMemset(c->split_flags, 0, nf * sizeof(int)) != hipSuccess)
@@ -567,6 +580,9 @@ int fpm_run(fpm_ctx *c, int iters) {
         } else if (c->path == FPM_PATH_FUSED && c->fused_mr) {
             HIP_TRY(launch_fused_mr_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
+        } else if (c->path == FPM_PATH_FUSED && c->dist) {
+            HIP_TRY(launch_fused_dist(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev, c->prob.n_order, c->tw_np,
+                                      c->split_ks, c->dbg, c->xch, c->split_flags, c->stream));
         } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->split_ks,
@@ -620,9 +636,12 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipMemcpy(h, c->dbg, sizeof h, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemset(c->dbg, 0, sizeof h));
         const double steps = (double)iters * c->prob.n_order * c->st.B;
-        const char *names[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre", "max",
-                                      "P",      "A:rowIDFT",   "C:rowDFT",  "upd:body",    "B:loop",
-                                      "split:Fstores", "split:Fwait"};
+        const char *names_f[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre", "max",
+                                        "P",      "A:rowIDFT",   "C:rowDFT",  "upd:body",    "B:loop",
+                                        "split:Fstores", "split:Fwait"};
+        const char *names_d[kStamps] = {"gather", "A", "sync1", "B", "sync2", "C", "update", "sync3",
+                                        "merge+Opre", "max", "P", "-", "-"};
+        const char *const *names = c->dist ? names_d : names_f;
         for (int v = 0; v < 2; ++v) {
             fprintf(stderr, "[fpm stamps] cycles per LED step (%s wave view, mean over blocks):", v ? "last" : "first");
             for (int i = 0; i < kStamps; ++i) fprintf(stderr, " %s=%.0f", names[i], h[v * kStamps + i] / steps);
@@ -721,6 +740,7 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
     info->fused_kernel = c->path != FPM_PATH_FUSED ? FPM_KERNEL_GENERAL
                          : c->fused_small      ? FPM_KERNEL_FUSED_SMALL
                          : c->fused_mr         ? FPM_KERNEL_FUSED_NP200
+                         : c->dist             ? FPM_KERNEL_FUSED_NP256_DIST
                                                : FPM_KERNEL_FUSED_NP256;
     return FPM_OK;
 }

@@ -40,140 +40,12 @@
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
 #include "fused256.hpp"
+#include "fused_common.hpp"
+#include "fused_sync.hpp"
 #include "update.hpp"
 
 namespace fpm {
 
-namespace fz {
-constexpr int NP = 256;
-constexpr int NROWS = 64;           // FFT rows per patch (RPG = NROWS / groups per group)
-constexpr int MAXTAIL = 64;         // tail pixels (one owner thread each)
-constexpr int MAXTAILROWS = 8;
-constexpr int SK[6] = {0, 1, 2, 13, 14, 15};  // registers that can hold |kx| <= 47
-constexpr int KYOFF = 48;                     // sigma table covers ky in [-48, 47]
-}  // namespace fz
-
-struct FusedArgs {
-    DevState st;
-    const uint16_t *meas;       // [nS][B][x][t][m2] = I[t + 16 m2][x] (meas_layout, preprocess.hip)
-    const int *order, *x0, *y0;
-    const float2 *tw;           // exp(-2 pi i k / 256), k < 256
-    float2 *pscr;               // 1024-thread variant: lane-private parking of P and F
-                                // [B][2][6][NT] (registers freed across pass B)
-    int n_order;
-    int ky_lo, n_fft_rows;      // FFT rows ky_lo .. ky_lo + n_fft_rows - 1 (sigma 0..)
-    int n_tail_rows;
-    int tail_ky[fz::MAXTAILROWS];  // sigma = 64 + i
-    int n_tail_px;
-    int2 tail_px[fz::MAXTAIL];  // (ky, kx), sorted by row then kx
-    // tail row q holds pixels tail_px[p0 .. p0+np) with kx = kx0, kx0+1, ...
-    int tail_row_p0[fz::MAXTAILROWS], tail_row_np[fz::MAXTAILROWS], tail_row_kx0[fz::MAXTAILROWS];
-    // tiles of the spectrum's live band (fpm_state.hpp): every other tile is
-    // exactly 0 and never changes, so the kernel keeps maxima and dirty bits
-    // for these nbt tiles only (band tile k = (bty0 + k / nbx, btx0 + k % nbx));
-    // st.tdirty holds the band-indexed bits between launches
-    int btx0, bty0, nbx, nbt;
-    float rnbx;                 // 1 / nbx
-    unsigned long long *dbg;    // diagnostic phase stamps (FPM_STAMPS=1), else null
-    // split mode (NT 512, KS = 2 or 4 workgroups per patch, KS * B <= CUs):
-    // workgroup p owns column part p (256 / KS columns); handoffs through xch
-    // with device-scope flags
-    float2 *xch;                // [B][KS parts][2 LED parities][kXchHalf]: F partial | tail F partial
-    int *flags;                 // [B][KS]: part p's F partials of LED it published (it + 1);
-                                // then the abort flag, then [B][KS] XCC_ID + 1 of each part
-    int *abort_flag;            // a handoff timed out: every workgroup leaves.  Sticky: the
-                                // per-launch reset does not clear it, fpm_run reports it
-    int stall_led;              // FPM_DEBUG_SPLIT_STALL (tests only): the last part stops
-                                // publishing from this LED on, forcing the timeout path; -1 off
-};
-
-// split-mode exchange area per patch (float2): each part's F partials of the
-// 512 lanes (12 slots each, lane-major) and of the <= 64 tail pixels, double
-// buffered by LED parity (a part overwrites its LED-i buffer only at LED i+2,
-// after every partner has published LED i+1, i.e. has read LED i's partials)
-constexpr int kXchTF = 12 * 512, kXchHalf = kXchTF + 64;
-constexpr int xch_patch_elems(int ks) { return 2 * ks * kXchHalf; }
-
-// Handoff between the two workgroups of a patch (split mode).  Everything the
-// partner reads -- the exchange area, the updated spectrum window, the flags --
-// moves with device-coherent (sc1) loads and stores (relaxed agent-scope
-// atomics), so no L2 write-back or invalidate is needed; the partner may sit
-// on another XCD.  (Agent-scope release/acquire fences instead -- buffer_wbl2 /
-// buffer_inv on every handoff -- measured 3.4x slower: they flush and
-// invalidate the whole XCD L2 that the other patches' streams use.)
-//   publish: every wave waits for its own stores to be acknowledged, then one
-//            thread stores the flag.
-//   wait:    one thread polls the flag (s_sleep between polls) and gives up
-//            after ~1 s, raising abort_flag so the partner leaves too.
-// Co-located pair (both workgroups report the same XCC_ID): the XCD's L2 is
-// the coherence point, so stores stay plain (the L1 writes through) and loads
-// bypass the L1 only (sc0 buffer loads): L2 round trips instead of memory
-// round trips on the critical path between the two halves.
-// aux: bit 0 = sc0 (bypass the L1), bit 31 = volatile (keeps the compiler from
-// hoisting a polled load out of its loop or merging it with earlier reads)
-constexpr int kAuxL2Volatile = (int)(1u | (1u << 31));
-__device__ __forceinline__ float2 ld_l2(__amdgpu_buffer_rsrc_t r, int byte_off) {
-    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, kAuxL2Volatile));
-}
-__device__ __forceinline__ int ld_l2_i32(__amdgpu_buffer_rsrc_t r, int byte_off) {
-    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, kAuxL2Volatile);
-}
-__device__ __forceinline__ int xcc_id() {
-    int x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & 15;
-}
-__device__ __forceinline__ void handoff_publish(int *flag, int value, bool local) {
-#ifndef FPM_EXP_NOWAIT  // timing experiment only (racy)
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are acknowledged
-#endif
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (local) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-// wait until every other part's flag (flags[0..KS), part `me` excluded) has
-// reached `value`
-template <int KS>
-__device__ __forceinline__ bool handoff_wait(int *flags, int me, int value, int *abort_flag, int *okslot, bool local,
-                                             __amdgpu_buffer_rsrc_t rflag) {
-    if (threadIdx.x == 0) {
-        int ok = 1;
-#pragma unroll
-        for (int p = 0; p < KS; ++p) {
-            if (p == me || !ok) continue;
-            for (int spins = 0;
-                 (local ? ld_l2_i32(rflag, p * (int)sizeof(int))
-                        : __hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < value;
-                 ++spins) {
-                if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    ok = 0;
-                    break;
-                }
-                if (spins > (1 << 23)) {
-                    __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        *okslot = ok;
-    }
-    __syncthreads();
-    return *okslot != 0;
-}
-
-// measurement stream: read once per LED, so load it non-temporally and keep
-// L2 for the spectrum window the next LED re-reads
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
-    const u32x4_t v = __builtin_nontemporal_load((const u32x4_t *)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-__device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
 
 // Column parts: T (the row IDFTs of the box rows) is held in LDS one column
 // part at a time -- two halves of 128 columns walked in turn by the
@@ -939,39 +811,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 
 // ------------------------------------------------------------------ host side
 namespace {
-struct FusedGeom {
-    bool ok = false;
-    int ky_lo = 0, n_fft_rows = 0, n_tail_rows = 0, tail_ky[fz::MAXTAILROWS] = {0};
-    int n_tail_px = 0;
-    int2 tail_px[fz::MAXTAIL];
-    int nbp = 0;
-};
-
-FusedGeom fused_geometry(int np, int r) {
-    FusedGeom g;
-    // the tail tables (8 rows, 64 pixels) hold every box row beyond the 64 FFT
-    // rows up to r = 34 (r = 35 has 7 tail rows with more than 64 pixels)
-    if (np != fz::NP || r < 1 || r > 34) return g;
-    const int nb = 2 * r + 1;
-    const int nfft = nb < fz::NROWS ? nb : fz::NROWS;
-    const int extra = nb - nfft;
-    g.ky_lo = -r + extra / 2;  // the 64 central rows go to the FFT groups
-    g.n_fft_rows = nfft;
-    for (int ky = -r; ky <= r; ++ky) {
-        if (ky >= g.ky_lo && ky < g.ky_lo + nfft) continue;
-        if (g.n_tail_rows >= fz::MAXTAILROWS) return g;
-        g.tail_ky[g.n_tail_rows++] = ky;
-        for (int kx = -r; kx <= r; ++kx)
-            if (ky * ky + kx * kx <= r * r) {
-                if (g.n_tail_px >= fz::MAXTAIL) return g;
-                g.tail_px[g.n_tail_px++] = make_int2(ky, kx);
-            }
-    }
-    g.nbp = ((fz::NROWS + g.n_tail_rows) + 3) / 4 * 4;
-    g.ok = true;
-    return g;
-}
-
 size_t fused_lds_bytes(int nt, int ks, int nbt, int n_tail_rows) {
     const int ng = nt / 16, xt = nt > 512 ? 8 * XP : XTILE;
     const int tld = part_cols(ks) + 1;
@@ -980,17 +819,6 @@ size_t fused_lds_bytes(int nt, int ks, int nbt, int n_tail_rows) {
            (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
 
-struct Band {
-    int bty0, btx0, nbx, nbt;
-};
-Band band_of(const DevState &st) {
-    Band b;
-    b.bty0 = st.sy0 / kTile;
-    b.btx0 = st.sx0 / kTile;
-    b.nbx = st.sx1 / kTile - b.btx0 + 1;
-    b.nbt = b.nbx * (st.sy1 / kTile - b.bty0 + 1);
-    return b;
-}
 }  // namespace
 
 // Threads per workgroup of the fused kernel for this geometry: 512 (2 waves

@@ -1,0 +1,662 @@
+// fused_dist.hip -- the Np 256 LED-update iteration DISTRIBUTED over KS = 2,
+// 4 or 8 workgroups per patch (small batches: a 256-patch field strong-scaled
+// over 2 / 4 / 8 GPUs leaves 128 / 64 / 32 patches per GPU, and one workgroup
+// per patch would leave most of the 256 CUs idle; the LEDs of a patch are
+// strictly sequential, fpmMain.cpp:345-476, so only intra-patch parallelism
+// can fill the chip).
+//
+// Split mode (fpm_fused.hip) gives each workgroup a column part but keeps the
+// row passes and the object/pupil update redundant in every workgroup; here
+// every phase is partitioned, at the price of three handoffs per LED:
+//
+//   part p owns FFT rows i = p, p + KS, p + 2 KS, ... of the 64 (one per
+//   16-lane group), tail rows q = p (mod KS), and the column part
+//   [p 256/KS, (p+1) 256/KS).
+//   gather   O = spec (own rows, on the support), X = O P              (:358-364)
+//   A        row IDFTs of the own rows, all 256 outputs -> Tg (a per-patch
+//            T image in L2-resident global memory)                      (:365)
+//   sync 1   (also carries each part's max|P| partial of the previous LED)
+//   B        Tg[box rows][own columns] -> LDS, column IDFT, 1/Np^2,
+//            amplitude replacement, column DFT (pass B of fpm_fused.hip
+//            verbatim), box rows back to Tg                              (:365-394)
+//   sync 2
+//   C        row DFTs of the own rows from Tg (full input), pruned to the
+//            support columns -> F complete, no partial sums               (:394)
+//   update   object update of the own rows on the support (:405-447), pupil
+//            numerator (:457-464), tile maxima of |spec| in LDS
+//   sync 3   (carries the window's tile maxima / dirty bits)
+//   merge    every part folds the partners' window tiles into its LDS copy,
+//            so all parts hold identical tile maxima
+//   max      exact max|objF| (:460,467), redundant in every part (identical)
+//   P        P += num / max|objF| on the own rows (:468-475), max|P| partial
+//
+// Handoffs: one monotone flag per part (3 per LED); Tg, the tile
+// publications and the spectrum move with device-coherent policies (plain
+// stores + L1-bypassing loads when every part of the patch sits on one XCD --
+// the L2 is the coherence point -- sc1 otherwise), see fused_sync.hpp.
+// Tg needs no double buffering: in A and C a part touches only its own rows,
+// in B only its own columns, and every phase change is behind a handoff.
+#include <hip/hip_runtime.h>
+
+#include "dft16.hpp"
+#include "fpm_state.hpp"
+#include "fused256.hpp"
+#include "fused_common.hpp"
+#include "fused_sync.hpp"
+#include "update.hpp"
+
+namespace fpm {
+
+namespace {
+constexpr int kTgRows = fz::NROWS + fz::MAXTAILROWS;  // Tg rows: 64 FFT rows + tail rows
+constexpr int kWinTiles = 64;                         // window tiles published per part (<= 6 x 6 used)
+// per-patch distributed-mode area (float2): Tg, then KS x kWinTiles tile
+// publications (max, dirty flag), then KS max|P| partials
+constexpr size_t dist_patch_elems(int ks) { return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + ks; }
+}  // namespace
+
+template <int KS>
+__global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
+    using namespace fz;
+    constexpr int NT = 512, NG = 32, NW = 8;
+    constexpr int TH = NP / KS, TLD = TH + 1;          // own column part
+    constexpr int NOWN = NROWS / KS;                   // own FFT row slots (groups 0 .. NOWN-1)
+    constexpr int CB = TH / 4 < 16 ? TH / 4 : 16;      // pass-B block: columns (r8 % CB) + CB gg + 4 CB (r8 / CB)
+    constexpr int NBLK = TH / 4;
+    static_assert(KS == 2 || KS == 4 || KS == 8, "two, four or eight parts");
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int nrows = NROWS + a.n_tail_rows;
+    float2 *scr_all = sm;                           // NG * XTILE exchange tiles
+    float2 *th = scr_all + NG * XTILE;              // (nrows + 2) * TLD: own columns of T
+    float2 *tw2 = th + (nrows + 2) * TLD;           // [m][t] = W256^{m t}
+    float2 *tw = tw2 + 256;                         // W256^k
+    float2 *tailX = tw + 256;                       // MAXTAIL
+    float2 *tailF = tailX + MAXTAIL;                // MAXTAIL
+    float *red = (float *)(tailF + MAXTAIL);        // 48: clean / dirty / pupil maxima per wave
+    int *sig = (int *)(red + 48);                   // 96: T row of ky in [-48, 47], -1 outside the box
+    int2 *tpx = (int2 *)(sig + 96);                 // MAXTAIL tail pixels (ky, kx)
+    int *tpq = (int *)(tpx + MAXTAIL);              // MAXTAIL: tail row of each tail pixel
+    float *tmx = (float *)(tpq + MAXTAIL);          // nbt: max|spec| per band tile (upper bound if dirty)
+    unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits
+    int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // [0] pass-B block counter, [1] handoff result
+
+    const DevState &st = a.st;
+    const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
+    const int xrd = exch_rbase(t);
+    const int lane = tid & 63, w = tid >> 6;
+    // block k -> patch 8 (k / (8 KS)) + k % 8, part (k / 8) % KS: the parts of a
+    // patch land on one XCD under round-robin dispatch (a speed matter only)
+    const int hown = (int)((blockIdx.x >> 3) % KS);
+    const int b = (int)((blockIdx.x / (8 * KS)) * 8 + (blockIdx.x & 7));
+    if (b >= st.B) return;  // grid rounded up to 8 KS blocks (block-uniform)
+    float2 *area = a.xch + (size_t)b * dist_patch_elems(KS);
+    int *flg = a.flags + KS * b;
+    int *xccs = a.flags + KS * st.B + 1 + KS * b;
+    const int R = st.r, NB = st.nb, L = st.L;
+    float2 *scr = scr_all + g * XTILE;
+    const int nwords = (a.nbt + 31) >> 5;
+    constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
+
+    // ---- one-time setup
+    if (tid == 0) {
+#pragma unroll
+        for (int i = 0; i < MAXTAIL; ++i) {
+            tpx[i] = a.tail_px[i];
+            int q = 0;
+#pragma unroll
+            for (int k = 0; k < MAXTAILROWS; ++k)
+                if (k < a.n_tail_rows && a.tail_ky[k] == a.tail_px[i].x) q = k;
+            tpq[i] = q;
+        }
+    }
+    for (int i = tid; i < 256; i += NT) {
+        tw[i] = a.tw[i];
+        tw2[i] = a.tw[((i >> 4) * (i & 15)) & 255];
+    }
+    for (int i = tid; i < 96; i += NT) {
+        const int ky = i - KYOFF;
+        int s = -1;
+        if (ky >= -R && ky <= R) {
+            if (ky >= a.ky_lo && ky < a.ky_lo + a.n_fft_rows) s = ky - a.ky_lo;
+#pragma unroll
+            for (int q = 0; q < MAXTAILROWS; ++q)
+                if (q < a.n_tail_rows && a.tail_ky[q] == ky) s = NROWS + q;
+        }
+        sig[i] = s;
+    }
+    auto band_dy = [&](int k) { return (int)(((float)k + 0.5f) * a.rnbx); };
+    auto band_gtile = [&](int k) {
+        const int dy = band_dy(k);
+        return (a.bty0 + dy) * st.ntx + a.btx0 + (k - dy * a.nbx);
+    };
+    float *tmax_g = st.tmax + (size_t)b * st.ntx * st.nty;
+    unsigned *dirty_g = st.tdirty + (size_t)b * ((st.ntx * st.nty + 31) / 32);
+    for (int k = tid; k < a.nbt; k += NT) tmx[k] = tmax_g[band_gtile(k)];
+    for (int i = tid; i < nwords; i += NT) dirty[i] = dirty_g[i];
+
+    float2 *spec = st.spec + (size_t)b * L * L;
+    float2 *pup = st.pupil + (size_t)b * NB * NB;
+    // own FFT row of this group: i = hown + KS g
+    const int irow = hown + KS * g;
+    const int kyr = a.ky_lo + irow;
+    const bool ron = g < NOWN && irow < a.n_fft_rows;
+    float2 P[6];
+    unsigned inmask = 0;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int kx = slot_kx(t, s);
+        const bool in = ron && (kyr * kyr + kx * kx <= R * R);
+        inmask |= (in ? 1u : 0u) << s;
+        P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
+    }
+    __syncthreads();  // tpx / tpq / sig
+    const int zoff = nrows * TLD;
+    int roff[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int sg = sig[slot_kx(t, s) + KYOFF];
+        roff[s] = sg >= 0 ? sg * TLD : zoff;
+    }
+    for (int i = tid; i < TLD; i += NT) th[zoff + i] = make_float2(0.f, 0.f);
+    // tail pixel tid: this part owns it when its row q = tpq[tid] is q = hown (mod KS)
+    const bool towner = tid < a.n_tail_px && (tpq[tid] % KS) == hown;
+    const int2 tp = tid < a.n_tail_px ? tpx[tid] : make_int2(0, 0);
+    float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
+    float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
+    float pm = st.pmax[b];
+    float pmx_part = 0.f;  // this part's max|P|^2 of the last pupil phase
+
+    // ---- coherence of the patch's shared data (see fused_sync.hpp)
+    bool local = false;
+    if (tid == 0) {
+        const int mine = xcc_id() + 1;
+        __hip_atomic_store(xccs + hown, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool same = true;
+#pragma unroll
+        for (int p = 0; p < KS; ++p) {
+            if (p == hown) continue;
+            int other = 0;
+            for (int spins = 0;
+                 (other = __hip_atomic_load(xccs + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0; ++spins) {
+                if (spins > (1 << 23) || __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            same = same && other == mine;
+        }
+        ccnt[1] = same;
+    }
+    __syncthreads();
+    local = ccnt[1] != 0;
+    __syncthreads();
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc(area, 0, (int)(dist_patch_elems(KS) * sizeof(float2)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(spec, 0, L * L * (int)sizeof(float2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, KS * (int)sizeof(int), 0x00020000);
+    // partner-visible loads / stores: L1-bypassing (sc0) loads and plain
+    // stores inside one XCD, device-scope (sc1) both ways across XCDs
+    auto cld = [&](__amdgpu_buffer_rsrc_t r, int elem) {
+        const int off = elem * (int)sizeof(float2);
+        return __builtin_bit_cast(float2, local ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 1)
+                                                : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+    };
+    auto cst = [&](__amdgpu_buffer_rsrc_t r, int elem, float2 v) {
+        const int off = elem * (int)sizeof(float2);
+        const u32x2_t d = __builtin_bit_cast(u32x2_t, v);
+        if (local) __builtin_amdgcn_raw_buffer_store_b64(d, r, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b64(d, r, off, 0, 16);
+    };
+    int sync_no = 0;  // handoffs of this launch (flag values are 1, 2, 3, ...)
+    bool aborted = false;
+    auto handoff = [&]() {
+        ++sync_no;
+        handoff_publish(flg + hown, sync_no, local);
+        return handoff_wait<KS>(flg, hown, sync_no, a.abort_flag, ccnt + 1, local, rf);
+    };
+
+    unsigned long long acc[kStamps] = {};
+    unsigned long long prev = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+#define FPM_STAMP(i)                                                  \
+    if (a.dbg) {                                                      \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        acc[i] += now_ - prev;                                        \
+        prev = now_;                                                  \
+    }
+    auto soff = [](int s) { return 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); };
+    // window of LED `itn` in the centred spectrum: element offset of (ky, kx) = (0, 0)
+    auto wbase = [&](int itn) {
+        const int ln = a.order[itn];
+        return (a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2;
+    };
+    float2 Opre[6];
+    auto load_window = [&](int itn) {
+        const int wb = wbase(itn) + kyr * L + t;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) Opre[s] = ((inmask >> s) & 1) ? cld(rs, wb + soff(s)) : make_float2(0.f, 0.f);
+        if (towner) Ot = cld(rs, wbase(itn) + tp.x * L + tp.y);
+    };
+    if (a.n_order > 0) load_window(0);
+    const float epsn = st.eps * (float)(NP * NP);
+    const float epsn_im = st.eps_im * (float)(NP * NP);
+    unsigned *tmu = (unsigned *)tmx;
+
+    for (int it = 0; it < a.n_order; ++it) {
+        const int led = a.order[it];
+        const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
+        const int wb0 = yc * L + xc;
+        const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
+        Tw<true> wt;
+        wt.load(tw2, t);
+        float2 v[16], r[16];
+
+        // ---- gather + A: row IDFTs of the own rows, all 256 outputs to Tg (:358-365)
+        if (towner) tailX[tid] = pout(pmul(pin(Ot), pin(Pt)));
+        __syncthreads();  // tailX
+        FPM_STAMP(0)
+        if (g < NOWN) {  // group-uniform
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
+            idft256_in6<false>(v, r, scr, wt, t, xrd);
+            if (ron) {
+#pragma unroll
+                for (int m = 0; m < 16; ++m) cst(ra, irow * NP + t + 16 * m, r[m]);
+            }
+        }
+        // own tail rows: direct sums over the row's pixels for every column x
+        for (int q = hown; q < a.n_tail_rows; q += KS) {
+            const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
+            for (int x = tid; x < NP; x += NT) {
+                const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
+                pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
+                const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
+                pf2 s2 = {0.f, 0.f}, s3 = {0.f, 0.f};
+                int p = 0;
+                for (; p + 1 < np_; p += 2) {
+                    s2 += pmulc(pin(tailX[p0 + p]), wa);
+                    s3 += pmulc(pin(tailX[p0 + p + 1]), wb);
+                    wa = pmul(wa, wstep);
+                    wb = pmul(wb, wstep);
+                }
+                if (p < np_) s2 += pmulc(pin(tailX[p0 + p]), wa);
+                cst(ra, (NROWS + q) * NP + x, pout(s2 + s3));
+            }
+        }
+        FPM_STAMP(1)
+        // ---- sync 1, with this part's max|P| partial of the previous LED
+        if (it > 0 && tid == 0) {
+            float m2 = red[32];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) m2 = fmaxf(m2, red[32 + i]);
+            cst(ra, PMX_OFF + hown, make_float2(m2, 0.f));
+        }
+        if (!handoff()) {
+            aborted = true;
+            break;
+        }
+        if (it > 0) {  // max|P| of the previous LED's pupil over all parts (:415)
+            float m2 = 0.f;
+#pragma unroll
+            for (int p = 0; p < KS; ++p) m2 = fmaxf(m2, cld(ra, PMX_OFF + p).x);
+            pm = sqrtf(m2);
+        }
+        FPM_STAMP(2)
+
+        // ---- B: own columns of T from Tg, column IDFT, amplitude, DFT (:365-394)
+        for (int i = tid; i < nrows * TH; i += NT) {
+            const int row = i / TH, xl = i - row * TH;
+            th[row * TLD + xl] = cld(ra, row * NP + TH * hown + xl);
+        }
+        if (tid == 0) *ccnt = NW;
+        __syncthreads();
+        {
+            auto colx = [&](int r8) { return (r8 % CB) + CB * gg + 4 * CB * (r8 / CB); };
+            auto ldI = [&](int xl, uint4 (&n)[2]) {
+                const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * hown) * 16 + t) * 16);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
+            };
+            float2 tin[6];
+#pragma unroll
+            for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(w)];
+            int r8 = w;
+            if (r8 < NBLK) {
+#pragma unroll 1
+                for (;;) {
+                    const int xl = colx(r8);
+                    uint4 cI[2];
+                    int nx = 0;
+                    if (lane == 0) nx = atomicAdd(ccnt, 1);
+                    nx = __builtin_amdgcn_readfirstlane(nx);
+                    ldI(xl, cI);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) v[SK[s]] = tin[s];
+                    idft256_in6<false>(v, r, scr, wt, t, xrd);
+                    {
+                        const int xn = colx(nx < NBLK ? nx : r8);
+#pragma unroll
+                        for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
+                    }
+                    const unsigned iw[8] = {cI[0].x, cI[0].y, cI[0].z, cI[0].w, cI[1].x, cI[1].y, cI[1].z, cI[1].w};
+#pragma unroll
+                    for (int m2 = 0; m2 < 16; ++m2) {
+                        const float Iv = (float)((m2 & 1) ? (iw[m2 >> 1] >> 16) : (iw[m2 >> 1] & 0xffffu));
+                        const pf2 tt = pin(r[m2]) + (pf2){epsn, epsn_im};
+                        const float mag2 = __builtin_fmaf(tt.x, tt.x, tt.y * tt.y);
+                        v[m2] = pout(pin(r[m2]) * amp_scale(mag2, Iv));
+                    }
+                    float2 o[6];
+                    dft256_out6<false>(v, o, scr, wt, t, xrd);
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
+                    if (nx >= NBLK) break;
+                    r8 = nx;
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < nrows * TH; i += NT) {
+            const int row = i / TH, xl = i - row * TH;
+            cst(ra, row * NP + TH * hown + xl, th[row * TLD + xl]);
+        }
+        FPM_STAMP(3)
+        if (!handoff()) {  // ---- sync 2
+            aborted = true;
+            break;
+        }
+        FPM_STAMP(4)
+
+        // ---- C: row DFTs of the own rows (full input) -> F (:394)
+        float2 F[6];
+        if (g < NOWN) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = ron ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
+            dft256_out6<false>(v, F, scr, wt, t, xrd);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
+        }
+        // own tail pixels: a 16-lane group sums the 256 columns of the pixel's row
+        for (int pp = g; pp < a.n_tail_px; pp += NG) {
+            if ((tpq[pp] % KS) != hown) continue;  // group-uniform
+            const int2 px = tpx[pp];
+            const int row = NROWS + tpq[pp];
+            pf2 s2p = {0.f, 0.f};
+            pf2 wk = pin(tw[(t * (px.y + NP)) & (NP - 1)]);
+            const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                s2p += pmul(pin(cld(ra, row * NP + t + 16 * m)), wk);
+                if (m < 15) wk = pmul(wk, wstep);
+            }
+            float2 s2 = pout(s2p);
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                s2.x += __shfl_xor(s2.x, o, 64);
+                s2.y += __shfl_xor(s2.y, o, 64);
+            }
+            if (t == 0) tailF[pp] = s2;
+        }
+        __syncthreads();  // tailF
+        FPM_STAMP(5)
+
+        // ---- object update of the own rows (:405-447), pupil numerator (:457-464)
+        auto note = [&](int py, int px, float ao, float an) {
+            const int ti = ((py >> 4) - a.bty0) * a.nbx + ((px >> 4) - a.btx0);
+            const unsigned cur = tmu[ti];
+            if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
+            if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
+        };
+        if (ron) {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) {
+                float2 num;
+                float oa;
+                const float2 nv = slot_update(F[s], Opre[s], P[s], pm, st, num, oa);
+                scr[s * 16 + t] = num;
+                if ((inmask >> s) & 1) {
+                    cst(rs, wb0 + kyr * L + t + soff(s), nv);
+                    note(yc + kyr, xc + slot_kx(t, s), oa, cmag(nv));
+                }
+            }
+        }
+        if (towner) {
+            float oa;
+            const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
+            cst(rs, wb0 + tp.x * L + tp.y, nv);
+            note(yc + tp.x, xc + tp.y, oa, cmag(nv));
+        }
+        __syncthreads();  // tile maxima of this part's pixels
+        // publish the window's tiles (the only ones any part changed)
+        const int wty0 = (yc - R) >> 4, wtx0 = (xc - R) >> 4;
+        const int wnx = ((xc + R) >> 4) - wtx0 + 1, wnt = wnx * (((yc + R) >> 4) - wty0 + 1);
+        auto wtile = [&](int k) {  // band index of window tile k
+            const int dy = k / wnx;
+            return (wty0 + dy - a.bty0) * a.nbx + (wtx0 + k - dy * wnx - a.btx0);
+        };
+        if (tid < wnt) {
+            const int bk = wtile(tid);
+            cst(ra, TILES_OFF + hown * kWinTiles + tid,
+                make_float2(tmx[bk], __uint_as_float((dirty[bk >> 5] >> (bk & 31)) & 1u)));
+        }
+        FPM_STAMP(6)
+        if (!handoff()) {  // ---- sync 3
+            aborted = true;
+            break;
+        }
+        FPM_STAMP(7)
+        // merge: every part ends with the same maxima and dirty bits
+        if (tid < wnt) {
+            const int bk = wtile(tid);
+            float m = tmx[bk];
+            unsigned d = 0;
+#pragma unroll
+            for (int p = 0; p < KS; ++p) {
+                if (p == hown) continue;
+                const float2 e = cld(ra, TILES_OFF + p * kWinTiles + tid);
+                m = fmaxf(m, e.x);
+                d |= __float_as_uint(e.y);
+            }
+            tmx[bk] = m;
+            if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
+        }
+        if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
+        __syncthreads();
+        FPM_STAMP(8)
+
+        // ---- exact max|objF| (:460,467), identical in every part
+        float cm = 0.f, dm = 0.f;
+        for (int k = tid; k < a.nbt; k += NT) {
+            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
+            if (d) dm = fmaxf(dm, tmx[k]);
+            else cm = fmaxf(cm, tmx[k]);
+        }
+        cm = wave_max(cm);
+        dm = wave_max(dm);
+        if (lane == 0) {
+            red[w] = cm;
+            red[16 + w] = dm;
+        }
+        __syncthreads();
+        cm = red[0];
+        dm = red[16];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            cm = fmaxf(cm, red[i]);
+            dm = fmaxf(dm, red[16 + i]);
+        }
+        float omax = cm;
+        if (dm > cm) {
+            for (int k = w; k < a.nbt; k += NW) {
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;
+                const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
+                float mm = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int pp = lane + 64 * jj;
+                    mm = fmaxf(mm, cmag(cld(rs, (ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15))));
+                }
+                mm = wave_max(mm);
+                if (lane == 0) {
+                    tmx[k] = mm;
+                    atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
+                }
+            }
+            __syncthreads();
+            float m2 = 0.f;
+            for (int k = tid; k < a.nbt; k += NT)
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
+            m2 = wave_max(m2);
+            __syncthreads();
+            if (lane == 0) red[w] = m2;
+            __syncthreads();
+            omax = red[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
+        }
+        FPM_STAMP(9)
+        const float rom = 1.0f / omax;
+        // ---- P += num / max|objF| on the own rows (:468-475), max|P| partial (:415)
+        float pmx = 0.f;
+        if (ron) {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) {
+                const float2 n = scr[s * 16 + t];
+                P[s] = make_float2(P[s].x + n.x * rom, P[s].y + n.y * rom);
+                pmx = fmaxf(pmx, cabs2(P[s]));
+            }
+        }
+        if (towner) {
+            Pt = make_float2(Pt.x + NPt.x * rom, Pt.y + NPt.y * rom);
+            pmx = fmaxf(pmx, cabs2(Pt));
+        }
+        pmx = wave_max(pmx);
+        if (lane == 0) red[32 + w] = pmx;
+        FPM_STAMP(10)
+    }
+#undef FPM_STAMP
+    __syncthreads();  // red[32..]
+    if (a.dbg && tid == 0 && (hown == 0 || hown == KS - 1))
+        for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(hown ? kStamps : 0) + i], acc[i]);
+    // ---- write back: each part its own pupil rows and tail pixels; part 0
+    // the tile maxima (identical in every part) and max|P| over all parts
+    if (ron) {
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+            if ((inmask >> s) & 1) pup[(kyr + R) * NB + slot_kx(t, s) + R] = P[s];
+    }
+    if (towner) pup[(tp.x + R) * NB + tp.y + R] = Pt;
+    if (a.n_order > 0 && !aborted) {
+        if (tid == 0) {
+            float m2 = red[32];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) m2 = fmaxf(m2, red[32 + i]);
+            cst(ra, PMX_OFF + hown, make_float2(m2, 0.f));
+        }
+        if (handoff() && hown == 0 && tid == 0) {
+            float m2 = 0.f;
+#pragma unroll
+            for (int p = 0; p < KS; ++p) m2 = fmaxf(m2, cld(ra, PMX_OFF + p).x);
+            st.pmax[b] = sqrtf(m2);
+        }
+    }
+    if (hown == 0) {
+        for (int k = tid; k < a.nbt; k += NT) tmax_g[band_gtile(k)] = tmx[k];
+        for (int i = tid; i < nwords; i += NT) dirty_g[i] = dirty[i];
+    }
+    (void)pmx_part;
+    (void)pm;
+}
+
+// ------------------------------------------------------------------ host side
+size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
+    const int tld = fz::NP / ks + 1;
+    return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
+           48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
+}
+
+// distributed-mode area (float2 elements) for B patches
+size_t fused_dist_elems(int B, int ks) { return (size_t)B * dist_patch_elems(ks); }
+
+// Workgroups per patch of the distributed mode: the largest KS in {8, 4, 2}
+// with KS * B <= CUs (every part must be co-resident: cooperative launch),
+// or 0 (not used).  FPM_DIST=0 disables it; FPM_DIST=2/4/8 forces a count
+// that fits.
+int fused_dist_parts(int B, int n_cu, int r, int L) {
+    if (B < 1 || getenv("FPM_NO_DIST")) return 0;
+    const FusedGeom g = fused_geometry(fz::NP, r);
+    if (!g.ok || L % kTile) return 0;
+    auto fits = [&](int ks) { return 8 * ks * ((B + 7) / 8) <= n_cu; };
+    if (const char *e = getenv("FPM_DIST")) {
+        const int ks = atoi(e);
+        return (ks == 2 || ks == 4 || ks == 8) && fits(ks) ? ks : 0;
+    }
+    return fits(8) ? 8 : fits(4) ? 4 : fits(2) ? 2 : 0;
+}
+
+hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
+                             const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
+                             float2 *area, int *flags, hipStream_t s) {
+    const FusedGeom g = fused_geometry(st.np, st.r);
+    if (!g.ok || (ks != 2 && ks != 4 && ks != 8) || !area || !flags) return hipErrorInvalidValue;
+    if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
+        return hipErrorInvalidValue;
+    FusedArgs a{};
+    a.st = st;
+    a.meas = meas;
+    a.order = order_dev;
+    a.x0 = x0_dev;
+    a.y0 = y0_dev;
+    a.tw = tw_np;
+    a.n_order = n_order;
+    a.ky_lo = g.ky_lo;
+    a.n_fft_rows = g.n_fft_rows;
+    a.n_tail_rows = g.n_tail_rows;
+    for (int i = 0; i < fz::MAXTAILROWS; ++i) a.tail_ky[i] = g.tail_ky[i];
+    a.n_tail_px = g.n_tail_px;
+    for (int q = 0; q < fz::MAXTAILROWS; ++q) {
+        a.tail_row_p0[q] = a.tail_row_np[q] = a.tail_row_kx0[q] = 0;
+        for (int p = 0; p < g.n_tail_px && q < g.n_tail_rows; ++p)
+            if (g.tail_px[p].x == g.tail_ky[q]) {
+                if (a.tail_row_np[q] == 0) {
+                    a.tail_row_p0[q] = p;
+                    a.tail_row_kx0[q] = g.tail_px[p].y;
+                }
+                ++a.tail_row_np[q];
+            }
+    }
+    for (int i = 0; i < fz::MAXTAIL; ++i) a.tail_px[i] = i < g.n_tail_px ? g.tail_px[i] : make_int2(0, 0);
+    const Band bd = band_of(st);
+    a.bty0 = bd.bty0;
+    a.btx0 = bd.btx0;
+    a.nbx = bd.nbx;
+    a.nbt = bd.nbt;
+    a.rnbx = 1.0f / (float)a.nbx;
+    a.dbg = dbg;
+    a.xch = area;
+    a.flags = flags;
+    a.abort_flag = flags + ks * st.B;
+    a.stall_led = -1;
+    const size_t lds = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const void *fn = ks == 8   ? (const void *)k_fused_dist<8>
+                     : ks == 4 ? (const void *)k_fused_dist<4>
+                               : (const void *)k_fused_dist<2>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    // handoff counters and XCC ids restart at zero; the abort word is sticky
+    e = hipMemsetAsync(flags, 0, (size_t)ks * st.B * sizeof(int), s);
+    if (e == hipSuccess) e = hipMemsetAsync(flags + ks * st.B + 1, 0, (size_t)ks * st.B * sizeof(int), s);
+    if (e != hipSuccess) return e;
+    void *args[] = {&a};
+    return hipLaunchCooperativeKernel(fn, dim3(8 * ks * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
+}
+
+}  // namespace fpm

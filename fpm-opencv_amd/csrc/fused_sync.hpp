@@ -1,0 +1,88 @@
+// fused_sync.hpp -- device-coherent handoffs between the workgroups that
+// share one patch (split mode of fpm_fused.hip, the distributed kernel of
+// fused_dist.hip), and the streamed measurement load.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace fpm {
+
+// Handoff between the two workgroups of a patch (split mode).  Everything the
+// partner reads -- the exchange area, the updated spectrum window, the flags --
+// moves with device-coherent (sc1) loads and stores (relaxed agent-scope
+// atomics), so no L2 write-back or invalidate is needed; the partner may sit
+// on another XCD.  (Agent-scope release/acquire fences instead -- buffer_wbl2 /
+// buffer_inv on every handoff -- measured 3.4x slower: they flush and
+// invalidate the whole XCD L2 that the other patches' streams use.)
+//   publish: every wave waits for its own stores to be acknowledged, then one
+//            thread stores the flag.
+//   wait:    one thread polls the flag (s_sleep between polls) and gives up
+//            after ~1 s, raising abort_flag so the partner leaves too.
+// Co-located pair (both workgroups report the same XCC_ID): the XCD's L2 is
+// the coherence point, so stores stay plain (the L1 writes through) and loads
+// bypass the L1 only (sc0 buffer loads): L2 round trips instead of memory
+// round trips on the critical path between the two halves.
+// aux: bit 0 = sc0 (bypass the L1), bit 31 = volatile (keeps the compiler from
+// hoisting a polled load out of its loop or merging it with earlier reads)
+constexpr int kAuxL2Volatile = (int)(1u | (1u << 31));
+__device__ __forceinline__ float2 ld_l2(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, kAuxL2Volatile));
+}
+__device__ __forceinline__ int ld_l2_i32(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, kAuxL2Volatile);
+}
+__device__ __forceinline__ int xcc_id() {
+    int x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 15;
+}
+__device__ __forceinline__ void handoff_publish(int *flag, int value, bool local) {
+#ifndef FPM_EXP_NOWAIT  // timing experiment only (racy)
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are acknowledged
+#endif
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (local) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// wait until every other part's flag (flags[0..KS), part `me` excluded) has
+// reached `value`
+template <int KS>
+__device__ __forceinline__ bool handoff_wait(int *flags, int me, int value, int *abort_flag, int *okslot, bool local,
+                                             __amdgpu_buffer_rsrc_t rflag) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+#pragma unroll
+        for (int p = 0; p < KS; ++p) {
+            if (p == me || !ok) continue;
+            for (int spins = 0;
+                 (local ? ld_l2_i32(rflag, p * (int)sizeof(int))
+                        : __hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < value;
+                 ++spins) {
+                if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = 0;
+                    break;
+                }
+                if (spins > (1 << 23)) {
+                    __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        *okslot = ok;
+    }
+    __syncthreads();
+    return *okslot != 0;
+}
+
+// measurement stream: read once per LED, so load it non-temporally and keep
+// L2 for the spectrum window the next LED re-reads
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
+    const u32x4_t v = __builtin_nontemporal_load((const u32x4_t *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+}  // namespace fpm

@@ -120,6 +120,8 @@ typedef struct fpm_ctx fpm_ctx;
 #define FPM_KERNEL_FUSED_NP256  1  /* k_fused_iteration (Np 256, r <= 34)          */
 #define FPM_KERNEL_FUSED_NP200  2  /* k_fused_mr (Np 200)                          */
 #define FPM_KERNEL_FUSED_SMALL  3  /* k_fused_small (Np <= 96)                     */
+#define FPM_KERNEL_FUSED_NP256_DIST 4  /* k_fused_dist (Np 256, every phase distributed
+                                          over wg_per_patch workgroups; small batches) */
 
 /* Which path the context runs and its per-launch geometry. */
 typedef struct fpm_info {
@@ -128,8 +130,9 @@ typedef struct fpm_info {
     int32_t support_px;    /* pixels in the pupil support disk                  */
     int32_t device;
     size_t  device_bytes;  /* device memory owned by the context               */
-    int32_t wg_per_patch;  /* fused Np 256 path (split mode): 4 when 4*n_patch
-                              <= CUs, 2 when 2*n_patch <= CUs, else 1          */
+    int32_t wg_per_patch;  /* fused Np 256 path: workgroups per patch (1, or 2 /
+                              4 / 8 in split or distributed mode when
+                              wg_per_patch * n_patch <= CUs)                   */
     int32_t fused_kernel;  /* FPM_KERNEL_*                                      */
 } fpm_info;
 

@@ -65,10 +65,12 @@ def test_bench_kernel_256_patches_vs_oracle():
             assert e < 1e-5, (k, b, e)
 
 
-@pytest.mark.parametrize("ks", [2, 4])
-def test_metric_geometry_5_iterations_vs_oracle(ks):
-    """Five runFPM iterations at the metric geometry on 2 patches (split mode
-    with KS workgroups per patch), objCrop / objF / pupil vs the oracle."""
+@pytest.mark.parametrize("ks,dist", [(2, False), (4, False), (4, True), (8, True)],
+                         ids=["split2", "split4", "dist4", "dist8"])
+def test_metric_geometry_5_iterations_vs_oracle(ks, dist):
+    """Five runFPM iterations at the metric geometry on 2 patches (split or
+    distributed mode with KS workgroups per patch), objCrop / objF / pupil vs
+    the oracle."""
     import oracle_lib
     from tools.synth import make_stack
     geo = _metric()
@@ -76,7 +78,8 @@ def test_metric_geometry_5_iterations_vs_oracle(ks):
     stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], n_patch=2, seed=55)
     prob = fpm_amd.Problem(geo["np_"], geo["L"], order, geo["x0"], geo["y0"], geo["r"], geo["d1"], geo["d2"],
                            n_patch=2)
-    os.environ["FPM_SPLIT"] = str(ks)
+    env = {"FPM_DIST": str(ks)} if dist else {"FPM_SPLIT": str(ks), "FPM_NO_DIST": "1"}
+    os.environ.update(env)
     try:
         with fpm_amd.Solver(prob) as s:
             assert s.info().wg_per_patch == ks
@@ -85,7 +88,8 @@ def test_metric_geometry_5_iterations_vs_oracle(ks):
             s.run(5)
             out = s.download(support=False)
     finally:
-        os.environ.pop("FPM_SPLIT", None)
+        for k in env:
+            os.environ.pop(k, None)
     if "it5" not in _REF:  # the same reference for both KS
         _REF["it5"] = oracle_lib.run_fpm_batch(stack, order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"],
                                                geo["d1"], geo["d2"], 5, threads=2, objF=True)
@@ -93,5 +97,6 @@ def test_metric_geometry_5_iterations_vs_oracle(ks):
     for b in range(2):
         for k in ("objCrop", "objF", "pupil"):
             e = rel_l2(out[k][b], refs[k][b])
-            print(f"metric geometry, 5 iterations, KS {ks}, patch {b}, {k}: rel L2 {e:.2e}")
+            print(f"metric geometry, 5 iterations, {'dist' if dist else 'split'} KS {ks}, patch {b}, {k}: "
+                  f"rel L2 {e:.2e}")
             assert e < 1e-4, (k, b, e)

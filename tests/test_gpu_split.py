@@ -25,19 +25,29 @@ from tools.synth import grid_geometry, make_stack
 pytestmark = pytest.mark.gpu
 
 
-def _solve(prob, stack, iters, ks):
-    """ks: workgroups per patch to force (FPM_SPLIT / FPM_NO_SPLIT)."""
-    key = "FPM_NO_SPLIT" if ks == 1 else "FPM_SPLIT"
-    os.environ[key] = "1" if ks == 1 else str(ks)
+def _env(ks, dist):
+    """Environment forcing ks workgroups per patch in split mode (dist False)
+    or distributed mode (dist True); ks 1 = one workgroup per patch."""
+    if ks == 1:
+        return {"FPM_NO_SPLIT": "1", "FPM_NO_DIST": "1"}
+    return {"FPM_DIST": str(ks)} if dist else {"FPM_SPLIT": str(ks), "FPM_NO_DIST": "1"}
+
+
+def _solve(prob, stack, iters, ks, dist=False):
+    env = _env(ks, dist)
+    os.environ.update(env)
     try:
         with fpm_amd.Solver(prob) as s:
             info = s.info()
+            want = fpm_amd.KERNEL_FUSED_NP256_DIST if dist else fpm_amd.KERNEL_FUSED_NP256
+            assert info.fused_kernel == want
             s.upload(stack)
             s.init()
             s.run(iters)
             return info.wg_per_patch, s.download()
     finally:
-        os.environ.pop(key, None)
+        for k in env:
+            os.environ.pop(k, None)
 
 
 @pytest.mark.parametrize("r,nside,step,B,iters", [(33, 5, 20, 5, 2), (34, 3, 30, 9, 1), (10, 4, 24, 1, 3)],
@@ -78,27 +88,59 @@ def test_split4_matches_one_workgroup_and_oracle(r, nside, step, B, iters):
             assert rel_l2(out4[k][b], ref[k]) < tol, (k, b)
 
 
-@pytest.mark.parametrize("ks", [2, 4])
-def test_split_metric_geometry_many_handoffs(ks):
-    """293 LEDs of the metric geometry (one handoff per LED) on 3 patches:
-    split vs one workgroup per patch, both finite and non-trivial."""
+@pytest.mark.parametrize("ks,dist", [(2, False), (4, False), (2, True), (4, True), (8, True)],
+                         ids=["split2", "split4", "dist2", "dist4", "dist8"])
+def test_split_metric_geometry_many_handoffs(ks, dist):
+    """293 LEDs of the metric geometry (one to three handoffs per LED) on 3
+    patches: split / distributed vs one workgroup per patch, both finite and
+    non-trivial."""
     from test_gpu_configs import _probe_geometry, _tiled_stack
     p, x0, y0 = _probe_geometry("geometry_dogStomach_metric.json")
     Np, L, r = p["np"], p["nlarge"], p["na_radius"]
     order = np.arange(len(x0))
     stack, _ = _tiled_stack(Np, L, r, x0, y0, 3, 3, seed=11)
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=3, path=fpm_amd.PATH_FUSED)
-    wgs, outs = _solve(prob, stack, 1, ks)
+    wgs, outs = _solve(prob, stack, 1, ks, dist)
     wg1, out1 = _solve(prob, stack, 1, 1)
     assert (wgs, wg1) == (ks, 1)
     assert np.isfinite(outs["objCrop"]).all()
     for k in ("objF", "objCrop", "pupil"):
-        if ks == 2:
+        if ks == 2 and not dist:
             np.testing.assert_array_equal(outs[k], out1[k], err_msg=k)
         else:
             for b in range(3):
                 assert rel_l2(outs[k][b], out1[k][b]) < 2e-6, (k, b)
     assert rel_l2(outs["objCrop"][0], outs["objCrop"][1]) > 1e-3  # patches differ
+
+
+@pytest.mark.parametrize("ks", [2, 4, 8])
+@pytest.mark.parametrize("r,nside,step,B,iters", [(33, 5, 20, 5, 2), (34, 3, 30, 3, 1), (10, 4, 24, 1, 3)],
+                         ids=["r33_B5_it2", "r34_B3_it1", "r10_B1_it3"])
+def test_distributed_matches_one_workgroup_and_oracle(r, nside, step, B, iters, ks):
+    """Distributed mode (fused_dist.hip): rows, columns and the update
+    partitioned over KS workgroups.  F is formed by one full-input row DFT
+    instead of the sum of two half-input ones, so it agrees with the
+    one-workgroup kernel to fp32 rounding (bound in the assertion); it is
+    deterministic and matches the fp64 oracle."""
+    import oracle_lib
+    Np, L = 256, 512
+    x0, y0, order = grid_geometry(Np, L, nside, step)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=B, seed=9 + r)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=B, path=fpm_amd.PATH_FUSED)
+    wgd, outd = _solve(prob, stack, iters, ks, dist=True)
+    wgd2, outd2 = _solve(prob, stack, iters, ks, dist=True)
+    wg1, out1 = _solve(prob, stack, iters, 1)
+    assert (wgd, wgd2, wg1) == (ks, ks, 1)
+    for k in ("objF", "objCrop", "pupil"):
+        np.testing.assert_array_equal(outd[k], outd2[k], err_msg=k)
+        for b in range(B):
+            e = rel_l2(outd[k][b], out1[k][b])
+            assert e < 2e-6, (k, b, e)
+    tol = 1e-5 if iters == 1 else 5e-5
+    for b in sorted({0, B - 1}):
+        ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, 10, 3, iters)
+        for k in ("objF", "objCrop", "pupil"):
+            assert rel_l2(outd[k][b], ref[k]) < tol, (k, b)
 
 
 def test_split_handoff_timeout_is_reported_and_sticky():
@@ -110,7 +152,12 @@ def test_split_handoff_timeout_is_reported_and_sticky():
     x0, y0, order = grid_geometry(Np, L, 3, 24)
     stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=3)
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=1, path=fpm_amd.PATH_FUSED)
-    with fpm_amd.Solver(prob) as s:
+    os.environ["FPM_NO_DIST"] = "1"  # split mode carries the stall knob
+    try:
+        s = fpm_amd.Solver(prob)
+    finally:
+        os.environ.pop("FPM_NO_DIST", None)
+    with s:
         assert s.info().wg_per_patch == 4
         s.upload(stack)
         s.init()

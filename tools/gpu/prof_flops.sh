@@ -15,4 +15,4 @@ for f in glob.glob(sys.argv[1] + "/p1/**/*counter_collection.csv", recursive=Tru
 for k, d in sorted(acc.items()):
     print(k, {c: int(v) for c, v in sorted(d.items())})
 PY
-grep expected $OUT/flops.log
+grep expected $OUT/flops.log; rm -rf $OUT/p1/

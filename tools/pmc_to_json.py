@@ -44,6 +44,9 @@ def short(name):
     m = re.search(r"k_fused_iteration<(\d+),\s*(\d+)>", name)
     if m:
         return f"k_fused_iteration<{m.group(1)},{m.group(2)}>"
+    m = re.search(r"k_fused_dist<(\d+)>", name)
+    if m:
+        return f"k_fused_dist<{m.group(1)}>"
     for k in ("k_fused_mr", "k_fused_small", "k_meas_layout", "k_meas_transpose_tiles", "k_meas_transpose",
               "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows600", "k_crop_cols600", "k_crop_rows",
               "k_crop_cols", "k_colpass_wave", "k_colpass_tiled", "k_gather_rowifft_tiled",
