@@ -61,6 +61,8 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
                              float2 *area, int *flags, hipStream_t s);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
+bool meas_layout_copy(const uint16_t *src, uint16_t *dst, int np, int g, size_t nimg, hipStream_t s,
+                      hipError_t *err);
 hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int B, const int *px0_dev,
                                    const int *py0_dev, int bk1x, int bk1y, int bk2x, int bk2y, double bg_threshold,
                                    double dark_mult, bool darkfield, unsigned long long *sums, uint16_t *out,
@@ -443,6 +445,17 @@ int fpm_upload_stack_device(fpm_ctx *c, const uint16_t *meas) {
     if (!c || !meas) return set_err(FPM_ERR_INVAL, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     const size_t n = (size_t)c->prob.n_stack * c->st.B * c->st.np * c->st.np;
+    if (c->meas_g && meas != c->meas) {
+        // the fused layouts of Np 256 / 200: copy and permute in one pass
+        hipError_t e = hipSuccess;
+        if (meas_layout_copy(meas, c->meas, c->st.np, c->meas_g, (size_t)c->prob.n_stack * c->st.B, c->stream, &e)) {
+            HIP_TRY(e);
+            c->st.meas_g = c->meas_g;
+            c->uploaded = true;
+            c->initialized = false;
+            return FPM_OK;
+        }
+    }
     HIP_TRY(hipMemcpyAsync(c->meas, meas, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, c->stream));
     return after_upload(c);
 }

@@ -196,4 +196,64 @@ hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hip
     return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------
+// Out-of-place layout: the device-to-device upload and the permutation in ONE
+// pass (fpm_upload_stack_device of the fused Np 256 / Np 200 paths): read the
+// caller's C-ABI stack once, write the column layout once -- 4 B of HBM per
+// pixel instead of the 8 B of a copy followed by the in-place permutation.
+// One block per CW-column strip of one image: the strip (Np rows x CW
+// columns) is staged in LDS with 8-byte loads, then every lane writes one
+// (x, t) run of R pixels with 8-byte stores (contiguous per wave).  The LDS
+// row pitch LD = CW + 4 makes the stride-G column reads conflict-free (rows
+// t + G m of 16 lanes land on 16 distinct even dword banks, the x pair on +0/+1).
+namespace {
+template <int NP, int G, int CW>
+__global__ void __launch_bounds__(256) k_meas_layout_copy(const uint16_t *__restrict__ src,
+                                                         uint16_t *__restrict__ dst, size_t nimg) {
+    constexpr int R = NP / G, LD = CW + 4, NS = NP / CW;
+    static_assert(NP % CW == 0 && CW % 4 == 0 && R % 4 == 0, "strip and run widths");
+    __shared__ __attribute__((aligned(8))) uint16_t tl[NP * LD];
+    const size_t img = blockIdx.x / NS;
+    const int x0 = (blockIdx.x % NS) * CW;
+    if (img >= nimg) return;
+    const uint16_t *p = src + img * NP * NP;
+    for (int i = threadIdx.x; i < NP * (CW / 4); i += 256) {
+        const int y = i / (CW / 4), c = i - y * (CW / 4);
+        *(uint2 *)&tl[y * LD + 4 * c] = *(const uint2 *)&p[y * NP + x0 + 4 * c];
+    }
+    __syncthreads();
+    uint16_t *q = dst + img * NP * NP + (size_t)x0 * NP;
+    for (int i = threadIdx.x; i < CW * G; i += 256) {
+        const int xl = i / G, t = i - xl * G;  // run (x0 + xl, t): pixels y = t + G m
+        uint16_t v[R];
+#pragma unroll
+        for (int m = 0; m < R; ++m) v[m] = tl[(t + G * m) * LD + xl];
+#pragma unroll
+        for (int k = 0; k < R / 4; ++k)
+            *(uint2 *)&q[xl * NP + t * R + 4 * k] =
+                make_uint2((unsigned)v[4 * k] | ((unsigned)v[4 * k + 1] << 16),
+                           (unsigned)v[4 * k + 2] | ((unsigned)v[4 * k + 3] << 16));
+    }
+}
+}  // namespace
+
+// stack [nimg][Np][Np] (C ABI, device) -> dst in the fused column layout;
+// false when (np, g) has no out-of-place kernel (callers copy + permute in place)
+bool meas_layout_copy(const uint16_t *src, uint16_t *dst, int np, int g, size_t nimg, hipStream_t s,
+                      hipError_t *err) {
+    *err = hipSuccess;
+    if (nimg == 0) return np == 256 && g == 16;
+    if (np == 256 && g == 16) {
+        hipLaunchKernelGGL((k_meas_layout_copy<256, 16, 64>), dim3((unsigned)(nimg * 4)), dim3(256), 0, s, src, dst,
+                           nimg);
+    } else if (np == 200 && g == 10) {
+        hipLaunchKernelGGL((k_meas_layout_copy<200, 10, 40>), dim3((unsigned)(nimg * 5)), dim3(256), 0, s, src, dst,
+                           nimg);
+    } else {
+        return false;
+    }
+    *err = hipGetLastError();
+    return true;
+}
+
 }  // namespace fpm
