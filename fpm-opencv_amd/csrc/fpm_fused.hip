@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     // plain pointers the 13 P stores had their addresses spilled to scratch,
     // each store paying a reload and a vmcnt(0): 9k cycles per LED).
     // cache policy: sc1 (16) when the partner is on another XCD; loads are
-    // volatile (bit 31) and bypass the L1 (sc0) when it shares this one.
+    // volatile (bit 31) and bypass the L1 (sc1) when it shares this one.
     typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
     const int lane_off = tid * (int)sizeof(float2);
     auto xst = [&](int slot, float2 v) {  // slot: the lane-independent part of the index

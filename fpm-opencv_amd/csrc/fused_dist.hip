@@ -196,12 +196,11 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         __builtin_amdgcn_make_buffer_rsrc(area, 0, (int)(dist_patch_elems(KS) * sizeof(float2)), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(spec, 0, L * L * (int)sizeof(float2), 0x00020000);
     const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, KS * (int)sizeof(int), 0x00020000);
-    // partner-visible loads / stores: L1-bypassing (sc0) loads and plain
-    // stores inside one XCD, device-scope (sc1) both ways across XCDs
+    // partner-visible loads / stores: every load L1-bypassing (sc1, served by
+    // the L2 or memory); stores plain inside one XCD (the line stays in the
+    // shared L2), device-scope write-through (sc1) across XCDs
     auto cld = [&](__amdgpu_buffer_rsrc_t r, int elem) {
-        const int off = elem * (int)sizeof(float2);
-        return __builtin_bit_cast(float2, local ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 1)
-                                                : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+        return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, elem * (int)sizeof(float2), 0, 16));
     };
     auto cst = [&](__amdgpu_buffer_rsrc_t r, int elem, float2 v) {
         const int off = elem * (int)sizeof(float2);

@@ -17,13 +17,18 @@ namespace fpm {
 //            thread stores the flag.
 //   wait:    one thread polls the flag (s_sleep between polls) and gives up
 //            after ~1 s, raising abort_flag so the partner leaves too.
-// Co-located pair (both workgroups report the same XCC_ID): the XCD's L2 is
-// the coherence point, so stores stay plain (the L1 writes through) and loads
-// bypass the L1 only (sc0 buffer loads): L2 round trips instead of memory
-// round trips on the critical path between the two halves.
-// aux: bit 0 = sc0 (bypass the L1), bit 31 = volatile (keeps the compiler from
-// hoisting a polled load out of its loop or merging it with earlier reads)
-constexpr int kAuxL2Volatile = (int)(1u | (1u << 31));
+// Co-located parts (every workgroup reports the same XCC_ID): the XCD's L2
+// is the coherence point, so stores stay plain (the L1 writes through and the
+// line stays in that L2) and loads bypass the L1 with the sc1 policy: L2
+// round trips instead of memory round trips on the critical path.  (An sc0
+// load is NOT enough: it hits the CU's L1 like a plain load, and the L1 is
+// never refreshed by other CUs' stores -- MI355X_MICROARCH.md, visibility
+// row; round 2 used sc0 here and was exposed as stale reads once the
+// distributed kernel re-read the same lines every LED.)
+// aux: bit 4 = sc1 (L1 bypass, L2-served), bit 31 = volatile (keeps the
+// compiler from hoisting a polled load out of its loop or merging it with
+// earlier reads)
+constexpr int kAuxL2Volatile = (int)(16u | (1u << 31));
 __device__ __forceinline__ float2 ld_l2(__amdgpu_buffer_rsrc_t r, int byte_off) {
     return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, kAuxL2Volatile));
 }
