@@ -306,9 +306,26 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         FPM_STAMP(2)
 
         // ---- B: own columns of T from Tg, column IDFT, amplitude, DFT (:365-394)
-        for (int i = tid; i < nrows * TH; i += NT) {
-            const int row = i / TH, xl = i - row * TH;
-            th[row * TLD + xl] = cld(ra, row * NP + TH * hown + xl);
+        {   // 16-byte loads, all issued before the first LDS write (one L2
+            // round trip, not one per row: the per-row loop measured 13k cycles)
+            constexpr int NQ2 = TH / 2, NLD = (kTgRows * NQ2 + NT - 1) / NT;
+            typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+            u32x4_t q[NLD];
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int i = tid + NT * k, row = i / NQ2, c2 = i - row * NQ2;
+                q[k] = i < nrows * NQ2 ? __builtin_amdgcn_raw_buffer_load_b128(
+                                             ra, (row * NP + TH * hown + 2 * c2) * (int)sizeof(float2), 0, 16)
+                                       : (u32x4_t){0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int i = tid + NT * k, row = i / NQ2, c2 = i - row * NQ2;
+                if (i < nrows * NQ2) {
+                    th[row * TLD + 2 * c2] = make_float2(__uint_as_float(q[k].x), __uint_as_float(q[k].y));
+                    th[row * TLD + 2 * c2 + 1] = make_float2(__uint_as_float(q[k].z), __uint_as_float(q[k].w));
+                }
+            }
         }
         if (tid == 0) *ccnt = NW;
         __syncthreads();
@@ -360,9 +377,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             }
         }
         __syncthreads();
-        for (int i = tid; i < nrows * TH; i += NT) {
-            const int row = i / TH, xl = i - row * TH;
-            cst(ra, row * NP + TH * hown + xl, th[row * TLD + xl]);
+        for (int i = tid; i < nrows * (TH / 2); i += NT) {  // 16-byte stores
+            const int row = i / (TH / 2), c2 = i - row * (TH / 2);
+            const float2 e0 = th[row * TLD + 2 * c2], e1 = th[row * TLD + 2 * c2 + 1];
+            typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+            const u32x4_t d = {__float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e1.x), __float_as_uint(e1.y)};
+            const int off = (row * NP + TH * hown + 2 * c2) * (int)sizeof(float2);
+            if (local) __builtin_amdgcn_raw_buffer_store_b128(d, ra, off, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b128(d, ra, off, 0, 16);
         }
         FPM_STAMP(3)
         if (!handoff()) {  // ---- sync 2
@@ -450,7 +472,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             break;
         }
         FPM_STAMP(7)
+        // the next window first (its loads overlap the merge), then the
         // merge: every part ends with the same maxima and dirty bits
+        if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
         if (tid < wnt) {
             const int bk = wtile(tid);
             float m = tmx[bk];
@@ -465,7 +489,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             tmx[bk] = m;
             if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
         }
-        if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
         __syncthreads();
         FPM_STAMP(8)
 
