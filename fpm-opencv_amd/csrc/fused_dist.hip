@@ -607,10 +607,14 @@ size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
 // distributed-mode area (float2 elements) for B patches
 size_t fused_dist_elems(int B, int ks) { return (size_t)B * dist_patch_elems(ks); }
 
-// Workgroups per patch of the distributed mode: the largest KS in {8, 4, 2}
-// with KS * B <= CUs (every part must be co-resident: cooperative launch),
-// or 0 (not used).  FPM_DIST=0 disables it; FPM_DIST=2/4/8 forces a count
-// that fits.
+// Workgroups per patch of the distributed mode: KS = 8 when 8 B <= CUs, 4 when
+// 4 B <= CUs (every part must be co-resident: cooperative launch), else 0 (not
+// used).  Measured on MI355X at the metric geometry: 32
+// patches 5.32 ms per iteration (split mode KS 4: 5.66), 64 patches 5.54
+// (split 5.66); at 128 patches the two-part version is SLOWER than split
+// mode (7.17 vs 6.71 ms: T crosses the L2 four times per LED), so KS = 2 is
+// only used when forced.  FPM_NO_DIST=1 disables it; FPM_DIST=2/4/8 forces
+// a count that fits.
 int fused_dist_parts(int B, int n_cu, int r, int L) {
     if (B < 1 || getenv("FPM_NO_DIST")) return 0;
     const FusedGeom g = fused_geometry(fz::NP, r);
@@ -620,7 +624,7 @@ int fused_dist_parts(int B, int n_cu, int r, int L) {
         const int ks = atoi(e);
         return (ks == 2 || ks == 4 || ks == 8) && fits(ks) ? ks : 0;
     }
-    return fits(8) ? 8 : fits(4) ? 4 : fits(2) ? 2 : 0;
+    return fits(8) ? 8 : fits(4) ? 4 : 0;
 }
 
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
