@@ -13,20 +13,27 @@ namespace fpm {
 // packed FP32: with D = Objfup - ObjfcropP (:409),
 //   O' = O + D conj(P) |P| / ((|P|^2 + d2 + i d2im) max|P|)      (:406-419,433)
 //   num = D conj(O) |O| / (|O|^2 + d1 + i d1im)  (/ max|objF| at the commit)
-// 1/((a + ic) m) = (a - ic) / ((a^2 + c^2) m) and the real factor |P| (|O|)
-// is folded into that coefficient.  |X| is cmag (the tile maxima's function).
+// The complex reciprocal is taken scale-safely: with a = |X|^2 + delta and
+// q = c / a, 1 / ((a + ic) m) = (1 - iq) / (a (1 + q^2) m), so no intermediate
+// exceeds a (the form (a - ic) / ((a^2 + c^2) m) squares a = |O|^2 + d1, i.e.
+// |O|^4, which overflows fp32 once |O| reaches ~3e9).  The real factor |P|
+// (|O|) is folded into the coefficient.  |X| is cmag (the tile maxima's function).
+__device__ __forceinline__ float2 upd_coef_safe(float a, float c, float m, float f) {
+    const float ri = __builtin_amdgcn_rcpf(a);
+    const float q = c * ri;
+    const float s = __builtin_amdgcn_rcpf(__builtin_fmaf(q, q, 1.0f) * m) * (ri * f);
+    return make_float2(s, -q * s);
+}
 __device__ __forceinline__ float2 slot_update(float2 f, float2 o, float2 p, float pm, const DevState &st,
                                               float2 &num, float &oa) {
     const pf2 po = pin(o), pp = pin(p);
     const pf2 D = pin(f) - pmul(po, pp);
     const float pa = cmag(p);
-    const float ap = __builtin_fmaf(pa, pa, st.delta2);
-    const float rp = __builtin_amdgcn_rcpf(__builtin_fmaf(ap, ap, st.d2_im * st.d2_im) * pm) * pa;
-    const pf2 nv = po + pmul(pmulc(D, pp), (pf2){ap * rp, -st.d2_im * rp});
+    const float2 cp = upd_coef_safe(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm, pa);
+    const pf2 nv = po + pmul(pmulc(D, pp), pin(cp));
     oa = cmag(o);
-    const float ao = __builtin_fmaf(oa, oa, st.delta1);
-    const float ro = __builtin_amdgcn_rcpf(__builtin_fmaf(ao, ao, st.d1_im * st.d1_im)) * oa;
-    num = pout(pmul(pmulc(D, po), (pf2){ao * ro, -st.d1_im * ro}));
+    const float2 co = upd_coef_safe(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f, oa);
+    num = pout(pmul(pmulc(D, po), pin(co)));
     return pout(nv);
 }
 

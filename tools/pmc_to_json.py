@@ -8,20 +8,26 @@ launch).  The output is stamped with tools/srchash.py's hash of the csrc tree
 it was measured on; bench.py ignores a file whose hash differs.
 
 Units and corrections (MI355X_MICROARCH.md, HBM [CDNA4] and PMC notes):
-  * FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE reports half the
-    bytes of 16-B/lane coalesced reads; other widths are uncalibrated.
-    The fused kernels' measurement and spectrum reads are 16-B/lane, so their
-    FETCH is doubled.  k_meas_layout (the one-time in-place layout change)
-    reads exactly n_img * Np^2 * 2 bytes with 2-B/lane reads; its FETCH ratio
-    is reported as a check of the counter, not applied.
+  * FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE = TCC_EA0_RDREQ x
+    64 B while the L2 issues 128-B requests, so it reports half the bytes.
+    When the request-size pass (TCC_EA0_RDREQ_32B/_64B/_128B) is present the
+    read bytes are 32 n32 + 64 n64 + 128 n128 -- calibrated on
+    k_meas_layout_copy, which reads exactly n_img Np^2 2 bytes (75008 images:
+    9.830e9 B predicted, 128 x 7.681e7 = 9.832e9 B counted); otherwise FETCH is
+    doubled.
   * GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = value / 8.
   * SQ_INSTS_VALU counts wave instructions; a wave64 FP32 VALU instruction
     occupies its SIMD for 2 cycles, so VALU issue fraction =
     2 * SQ_INSTS_VALU / (1024 SIMDs * kernel cycles).
   * SQ_WAVE_CYCLES, SQ_ACTIVE_INST_*, SQ_WAIT_* count quad-cycles; ratios
     between them are unit-free.
-  * FP32 flops executed = 64 lanes * (2 FMA + ADD + MUL + TRANS) wave
-    instructions of the SQ_INSTS_VALU_*_F32 counters (when collected).
+  * FP32 flops counted = 64 lanes * (2 FMA + ADD + MUL + TRANS) wave
+    instructions of the SQ_INSTS_VALU_*_F32 counters (when collected).  These
+    count a PACKED instruction once, like its scalar form
+    (tools/gpu/micro/flop_count.hip: 2^26 v_pk_fma_f32 -> 2^26 FMA_F32 on
+    MI355X, profiles/r03_flop_count.txt), so for the packed-FP32 fused
+    kernels fp32_flops is half of the flops executed by the packed part:
+    fp32_flops_packed_upper (2x) bounds the executed flops from above.
 """
 import csv
 import glob
@@ -70,6 +76,7 @@ def derive(c):
         if all(v is not None for v in f32):
             fl = 64.0 * (2 * f32[0] + f32[1] + f32[2] + f32[3])
             d["fp32_flops"] = fl
+            d["fp32_flops_packed_upper"] = 2.0 * fl
             d["fp32_flops_per_cycle_frac"] = fl / (N_SIMD * 64.0 * cyc)
     wc = c.get("SQ_WAVE_CYCLES")
     if wc:
@@ -86,28 +93,38 @@ def main():
     src, out = sys.argv[1], sys.argv[2]
     acc = defaultdict(lambda: defaultdict(list))
     perm = []  # (work-items, FETCH bytes) per k_meas_layout dispatch
-    for f in sorted(glob.glob(os.path.join(src, "*", "**", "*counter_collection.csv"), recursive=True)):
-        with open(f) as fh:
-            for r in csv.DictReader(fh):
-                k = short(r["Kernel_Name"])
-                v = float(r["Counter_Value"])
-                acc[k][r["Counter_Name"]].append(v)
-                if k == "k_meas_layout" and r["Counter_Name"] == "FETCH_SIZE" and "Grid_Size" in r:
-                    perm.append((int(r["Grid_Size"]), v * 1024.0))
-    raw = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
-    res = {"src_hash": src_hash(), "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
+    if src.endswith(".json"):  # re-reduce an earlier output (its raw means and stamp)
+        with open(src) as fh:
+            prev = json.load(fh)
+        raw, stamp = prev["raw_per_launch"], prev["src_hash"]
+    else:
+        for f in sorted(glob.glob(os.path.join(src, "*", "**", "*counter_collection.csv"), recursive=True)):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    k = short(r["Kernel_Name"])
+                    v = float(r["Counter_Value"])
+                    acc[k][r["Counter_Name"]].append(v)
+                    if k == "k_meas_layout" and r["Counter_Name"] == "FETCH_SIZE" and "Grid_Size" in r:
+                        perm.append((int(r["Grid_Size"]), v * 1024.0))
+        raw = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+        stamp = src_hash()
+    res = {"src_hash": stamp, "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
            "derived": {}}
-    if perm:
-        # grid n_img x 1024 threads, one Np 256 image (128 KiB) per block
-        np_ = 256
-        known = sum(g // 1024 * np_ * np_ * 2.0 for g, _ in perm)
+    if perm and "k_meas_layout" in raw and "TCC_EA0_RDREQ_128B" in raw["k_meas_layout"]:
+        # k_meas_layout_copy<256,16,64>: 4 blocks of 256 threads per Np 256 image (128 KiB read)
+        known = sum(g // 1024 * 256 * 256 * 2.0 for g, _ in perm) / len(perm)
+        r = raw["k_meas_layout"]
         res["layout_known_read_bytes"] = known
-        res["layout_fetch_ratio"] = known / sum(v for _, v in perm)
+        res["layout_counted_read_bytes"] = 128.0 * r["TCC_EA0_RDREQ_128B"] + 64.0 * r["TCC_EA0_RDREQ_64B"]
     for k, d in raw.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            scale = 2.0
-            res["read_scale"][k] = scale
-            res["per_launch_hbm_bytes"][k] = d["FETCH_SIZE"] * 1024.0 * scale + d["WRITE_SIZE"] * 1024.0
+            if all(c in d for c in ("TCC_EA0_RDREQ_32B", "TCC_EA0_RDREQ_64B", "TCC_EA0_RDREQ_128B")):
+                rd = 32.0 * d["TCC_EA0_RDREQ_32B"] + 64.0 * d["TCC_EA0_RDREQ_64B"] + 128.0 * d["TCC_EA0_RDREQ_128B"]
+                res["read_scale"][k] = rd / (d["FETCH_SIZE"] * 1024.0) if d["FETCH_SIZE"] else None
+            else:
+                rd = d["FETCH_SIZE"] * 1024.0 * 2.0
+                res["read_scale"][k] = 2.0
+            res["per_launch_hbm_bytes"][k] = rd + d["WRITE_SIZE"] * 1024.0
         dv = derive(d)
         if dv:
             res["derived"][k] = dv
