@@ -56,6 +56,16 @@ constexpr int SPC = WPB + 1;       // column-pass strip pitch (complex)
 static_assert(4 * 8 * CXP <= WTILE, "cross-group tile");
 }  // namespace n1k
 
+// R1 holds its row's loads in registers (hoisted ahead of the pupil stores):
+// 128 VGPRs = 4 waves per SIMD with a few spills (measured 38.5 -> 36.3 us per
+// launch at config 5), or 3 waves without (-DFPM_N1K_OCC3).  The same
+// hoisting in R2 measured slower (36.4 -> 40.0 us) and is not used.
+#ifdef FPM_N1K_OCC3
+#define FPM_N1K_ROWS_OCC
+#else
+#define FPM_N1K_ROWS_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+
 namespace {
 
 __device__ __forceinline__ void wave_sync() {
@@ -145,7 +155,7 @@ __device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__re
 // K4 left (:460,467), and the row's max|P| for this LED's update (:415) as
 // partial pmax[row] -- the same arithmetic as K5, so the results are
 // bit-identical; K5 itself then runs once, after the last LED.
-__global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw,
+__global__ void __launch_bounds__(n1k::NT) FPM_N1K_ROWS_OCC k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw,
                                                           int commit) {
     using namespace n1k;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
@@ -168,20 +178,31 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_inv(DevState st, StepArgs 
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;         // + kx (:358-362)
     float2 x[16];
     float pmx = 0.f;
+    // every load of the row first, then the arithmetic and the pupil stores:
+    // a store to pup between the loads made the compiler keep them in program
+    // order (pup may alias the spectrum and dP), one memory latency per j
+    float2 pv[16], dv[16], ov[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int kx = fold(4 * (t + 16 * j) + c);
+        const bool in = kx * kx <= w2;
+        pv[j] = in ? pup[kx] : make_float2(0.f, 0.f);
+        dv[j] = (in && commit) ? dP[kx] : make_float2(0.f, 0.f);
+        ov[j] = in ? spec_ld(st, b, srow + kx) : make_float2(0.f, 0.f);
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int kx = fold(4 * (t + 16 * j) + c);
         x[j] = make_float2(0.f, 0.f);
         if (kx * kx <= w2) {
-            float2 p = pup[kx];
+            float2 p = pv[j];
             if (commit) {
-                const float2 d = dP[kx];
-                p.x += d.x / omax;
-                p.y += d.y / omax;
+                p.x += dv[j].x / omax;
+                p.y += dv[j].y / omax;
                 pup[kx] = p;
             }
             pmx = fmaxf(pmx, cmag(p));
-            x[j] = cmul(spec_ld(st, b, srow + kx), p);  // :364
+            x[j] = cmul(ov[j], p);  // :364
         }
     }
     pmx = wave_max(pmx);
