@@ -217,9 +217,19 @@ __global__ void __launch_bounds__(256) k_meas_layout_copy(const uint16_t *__rest
     const int x0 = (blockIdx.x % NS) * CW;
     if (img >= nimg) return;
     const uint16_t *p = src + img * NP * NP;
-    for (int i = threadIdx.x; i < NP * (CW / 4); i += 256) {
-        const int y = i / (CW / 4), c = i - y * (CW / 4);
-        *(uint2 *)&tl[y * LD + 4 * c] = *(const uint2 *)&p[y * NP + x0 + 4 * c];
+    if constexpr (CW % 8 == 0) {  // 16-byte loads (two 8-byte LDS writes: rows are 8-B aligned)
+#pragma unroll 4
+        for (int i = threadIdx.x; i < NP * (CW / 8); i += 256) {
+            const int y = i / (CW / 8), c = i - y * (CW / 8);
+            const uint4 q = *(const uint4 *)&p[y * NP + x0 + 8 * c];
+            *(uint2 *)&tl[y * LD + 8 * c] = make_uint2(q.x, q.y);
+            *(uint2 *)&tl[y * LD + 8 * c + 4] = make_uint2(q.z, q.w);
+        }
+    } else {
+        for (int i = threadIdx.x; i < NP * (CW / 4); i += 256) {
+            const int y = i / (CW / 4), c = i - y * (CW / 4);
+            *(uint2 *)&tl[y * LD + 4 * c] = *(const uint2 *)&p[y * NP + x0 + 4 * c];
+        }
     }
     __syncthreads();
     uint16_t *q = dst + img * NP * NP + (size_t)x0 * NP;
@@ -228,11 +238,16 @@ __global__ void __launch_bounds__(256) k_meas_layout_copy(const uint16_t *__rest
         uint16_t v[R];
 #pragma unroll
         for (int m = 0; m < R; ++m) v[m] = tl[(t + G * m) * LD + xl];
+        auto pk = [&](int m) { return (unsigned)v[m] | ((unsigned)v[m + 1] << 16); };
+        if constexpr (R % 8 == 0) {  // 16-byte stores (runs of 32 B are 16-B aligned)
 #pragma unroll
-        for (int k = 0; k < R / 4; ++k)
-            *(uint2 *)&q[xl * NP + t * R + 4 * k] =
-                make_uint2((unsigned)v[4 * k] | ((unsigned)v[4 * k + 1] << 16),
-                           (unsigned)v[4 * k + 2] | ((unsigned)v[4 * k + 3] << 16));
+            for (int k = 0; k < R / 8; ++k)
+                *(uint4 *)&q[xl * NP + t * R + 8 * k] = make_uint4(pk(8 * k), pk(8 * k + 2), pk(8 * k + 4), pk(8 * k + 6));
+        } else {
+#pragma unroll
+            for (int k = 0; k < R / 4; ++k)
+                *(uint2 *)&q[xl * NP + t * R + 4 * k] = make_uint2(pk(4 * k), pk(4 * k + 2));
+        }
     }
 }
 }  // namespace
