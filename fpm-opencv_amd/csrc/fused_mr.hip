@@ -56,6 +56,11 @@ constexpr int RMAX = 29;
 constexpr int KYOFF = 32;                 // sig table covers ky in [-32, 31]
 constexpr int XP = 10;                    // exchange-tile row pitch (complex)
 constexpr int XT = 10 * XP;               // exchange tile per group (complex)
+// Group stride of the exchange tiles when LDS allows (r <= 28): 106 = 10 (mod
+// 32), so the 8-byte row writes of the three groups a 32-lane LDS batch holds
+// land on disjoint banks (106 * 2 dwords = 20 mod 64); with stride 100 they
+// overlapped two ways (the 16-byte row reads stay conflict-free either way).
+constexpr int kXtFast = 106;
 constexpr int TLD = NP + 1;               // T row pitch (complex)
 }  // namespace fm
 
@@ -68,6 +73,7 @@ struct FusedMRArgs {
     int btx0, bty0, nbx, nbt;  // live-band tiles (fpm_fused.hip FusedArgs)
     float rnbx;
     unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles, else null
+    int xt;                    // exchange-tile stride per group (complex): kXtFast or fm::XT
 };
 
 __device__ __forceinline__ int mr_slot_k(int s) { return fm::SK[s]; }
@@ -80,7 +86,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     const DevState &st = a.st;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *tiles = sm;                        // NG * XT exchange tiles
-    float2 *th = tiles + NG * XT;              // (NB + 2) * TLD: T rows, zero row, dummy row
+    float2 *th = tiles + NG * a.xt;            // (NB + 2) * TLD: T rows, zero row, dummy row
     float2 *tw2 = th + (NB + 2) * TLD;         // [m1][l] = W200^{l m1}
     float *red = (float *)(tw2 + 200);         // 48
     int *sig = (int *)(red + 48);              // 64: T row of ky in [-32, 31], -1 outside the box
@@ -94,7 +100,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     const int l = act ? lane - N2 * gw : 0;    // lane within the group
     const int g = w * GPW + (act ? gw : 0);    // group in the workgroup
     const int b = blockIdx.x;
-    float2 *tile = tiles + g * XT;
+    float2 *tile = tiles + g * a.xt;
     const int xrd = opaque_i(l * XP);
     const int nwords = (a.nbt + 31) >> 5;
 
@@ -368,8 +374,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 
 // ------------------------------------------------------------------ host side
 namespace {
-size_t mr_lds_bytes(int nb, int nbt) {
-    return (size_t)(fm::NG * fm::XT + (nb + 2) * fm::TLD + 200) * sizeof(float2) + 48 * sizeof(float) +
+size_t mr_lds_bytes(int nb, int nbt, int xt = fm::XT) {
+    return (size_t)(fm::NG * xt + (nb + 2) * fm::TLD + 200) * sizeof(float2) + 48 * sizeof(float) +
            64 * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) +
            sizeof(int);
 }
@@ -403,7 +409,8 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
     a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
     a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
-    const size_t lds = mr_lds_bytes(st.nb, a.nbt);
+    a.xt = (mr_lds_bytes(st.nb, a.nbt, fm::kXtFast) <= 160 * 1024 && !getenv("FPM_MR_XT100")) ? fm::kXtFast : fm::XT;
+    const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xt);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_mr, dim3(st.B), dim3(fm::NT), lds, s, a);

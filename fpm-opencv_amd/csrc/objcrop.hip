@@ -251,16 +251,21 @@ __global__ void __launch_bounds__(64 * W) k_crop_rows600(const float2 *__restric
 }
 
 // pass 2: column IDFTs in place, scaled 1/L^2, one strip of G = 6 W columns
-// per block staged through LDS in two halves of 300 rows (see k_crop_cols).
-// Half h holds input registers k in [10 h, 10 h + 10) (element 3 (l + 10 k) + c
-// >= 300 iff k >= 10) and output registers with 10 k + 200 p >= 300.
+// per block staged through LDS in NH pieces of L / NH rows (see k_crop_cols).
+// Piece h holds input registers k in [h K, (h + 1) K), K = 20 / NH (element
+// 3 (l + 10 k) + c, 3 l + c < 30, never straddles a piece boundary of a
+// multiple of 30 rows) and the output registers whose rows 10 k + 200 p + l
+// (l < 10) fall in it.  W 8 / NH 4: 48-column strips -- 384-byte row
+// segments, three whole 128-byte lines -- in 59 KB pieces, two blocks per
+// CU (round 2's 12-column strips moved 96-byte segments that straddle lines).
 // grid (ceil(L / G), B), block 64 W
-template <int W>
+template <int W, int NH>
 __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
                                                          float scale, int sy0, int sy1) {
-    constexpr int G = GPW * W, SP = G + 1;
+    constexpr int G = GPW * W, SP = G + 1, HH = L / NH, K = 20 / NH;
+    static_assert(L % NH == 0 && HH % 30 == 0 && 20 % NH == 0, "pieces of whole 30-row runs");
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    float2 *twL = sm, *tw2 = sm + L, *strip = tw2 + 200;  // H x SP
+    float2 *twL = sm, *tw2 = sm + L, *strip = tw2 + 200;  // HH x SP
     float2 *tiles = strip;  // exchange tiles inside the strip: used only while every column is in registers
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gw = lane / 10;
     const bool act = gw < GPW;
@@ -275,54 +280,57 @@ __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io
     constexpr int NTH = 64 * W;
     float2 x[3][20];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        // objF row y + h H is spec row y + (1 - h) H: live rows of this half
-        const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
+    for (int h = 0; h < NH; ++h) {
+        // objF row y (0 <= y < L) is spec row (y + H) mod L: the live rows of
+        // this piece [h HH, (h+1) HH) form the contiguous range [ya, yb]
+        // relative to the piece (HH divides H, so a piece never wraps)
+        const int s0 = h * HH >= H ? h * HH - H : h * HH + H;  // spec row of the piece's first row
+        const int ya = max(sy0 - s0, 0), yb = min(sy1 - s0, HH - 1);
         for (int idx = ya * G + threadIdx.x; idx < (yb + 1) * G; idx += NTH) {
             const int y = idx / G, cc = idx - y * G;
-            if (cc < ncol) strip[y * SP + cc] = base[(size_t)(y + h * H) * L + cc];
+            if (cc < ncol) strip[y * SP + cc] = base[(size_t)(y + h * HH) * L + cc];
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 10 * h; k < 10 * h + 10; ++k)
+        for (int k = K * h; k < K * h + K; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const int y = 3 * (l + 10 * k) + c - h * H;
+                const int y = 3 * (l + 10 * k) + c - h * HH;
                 x[c][k] = (colok && y >= ya && y <= yb) ? strip[y * SP + g] : make_float2(0.f, 0.f);
             }
         __syncthreads();
     }
     dft600_regs<true>(x, tile, tw2, twL, l, xrd);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        __syncthreads();  // exchange tiles / previous half's reads are done
+    for (int h = 0; h < NH; ++h) {
+        __syncthreads();  // exchange tiles / previous piece's reads are done
         if (colok) {
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
                 for (int k = 0; k < 20; ++k)
-                    if ((10 * k + 200 * p >= H) == (h == 1))
-                        strip[(l + 10 * k + 200 * p - h * H) * SP + g] = cscale(x[p][k], scale);
+                    if ((10 * k + 200 * p) / HH == h)
+                        strip[(l + 10 * k + 200 * p - h * HH) * SP + g] = cscale(x[p][k], scale);
         }
         __syncthreads();
-        for (int idx = threadIdx.x; idx < H * G; idx += NTH) {
+        for (int idx = threadIdx.x; idx < HH * G; idx += NTH) {
             const int y = idx / G, cc = idx - y * G;
-            if (cc < ncol) base[(size_t)(y + h * H) * L + cc] = strip[y * SP + cc];
+            if (cc < ncol) base[(size_t)(y + h * HH) * L + cc] = strip[y * SP + cc];
         }
     }
 }
 
-template <int WR, int WC>
+template <int WR, int WC, int NHC>
 hipError_t launch_crop600(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
     constexpr int GC = GPW * WC;
     const size_t lds_rows = (size_t)(L + 200 + (GPW * WR + 1) * 100) * sizeof(float2);
-    constexpr size_t strip =
-        (size_t)H * (GC + 1) > (size_t)(GC + 1) * 100 ? (size_t)H * (GC + 1) : (size_t)(GC + 1) * 100;
+    constexpr size_t strip = (size_t)(L / NHC) * (GC + 1) > (size_t)(GC + 1) * 100 ? (size_t)(L / NHC) * (GC + 1)
+                                                                                  : (size_t)(GC + 1) * 100;
     const size_t lds_cols = (L + 200 + strip) * sizeof(float2);
     hipError_t e = hipFuncSetAttribute((const void *)k_crop_rows600<WR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds_rows);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void *)k_crop_cols600<WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void *)k_crop_cols600<WC, NHC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_cols);
     if (e != hipSuccess) return e;
     if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1)
@@ -330,7 +338,7 @@ hipError_t launch_crop600(const DevState &st, float2 *out, const float2 *tw_L, h
     const int nrows = st.sy1 - st.sy0 + 1, gr = GPW * WR;
     hipLaunchKernelGGL(k_crop_rows600<WR>, dim3((nrows + gr - 1) / gr, st.B), dim3(64 * WR), lds_rows, s,
                        (const float2 *)st.spec, out, tw_L, st.sy0, st.sy1, st.sx0, st.sx1);
-    hipLaunchKernelGGL(k_crop_cols600<WC>, dim3((L + GC - 1) / GC, st.B), dim3(64 * WC), lds_cols, s, out, tw_L,
+    hipLaunchKernelGGL((k_crop_cols600<WC, NHC>), dim3((L + GC - 1) / GC, st.B), dim3(64 * WC), lds_cols, s, out, tw_L,
                        1.0f / ((float)L * (float)L), st.sy0, st.sy1);
     return hipGetLastError();
 }
@@ -352,7 +360,9 @@ hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw
         case 512: return launch_crop<2, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
         case 768: return launch_crop<3, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
         case 1024: return launch_crop<4, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
-        case 600: return c600::launch_crop600<1, 2>(st, out, tw_L, s);
+        case 600:
+            return getenv("FPM_CROP600_OLD") ? c600::launch_crop600<1, 2, 2>(st, out, tw_L, s)
+                                             : c600::launch_crop600<1, 8, 4>(st, out, tw_L, s);
         default: return hipErrorNotSupported;
     }
 }

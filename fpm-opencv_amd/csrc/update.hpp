@@ -19,6 +19,10 @@ namespace fpm {
 // |O|^4, which overflows fp32 once |O| reaches ~3e9).  The real factor |P|
 // (|O|) is folded into the coefficient.  |X| is cmag (the tile maxima's function).
 __device__ __forceinline__ float2 upd_coef_safe(float a, float c, float m, float f) {
+#ifdef FPM_UPD_SQUARED  // A/B only: round 2's (a - ic) / ((a^2 + c^2) m), one rcp, overflows at |X| ~ 3e9
+    const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(a, a, c * c) * m) * f;
+    return make_float2(a * r, -c * r);
+#endif
     const float ri = __builtin_amdgcn_rcpf(a);
     const float q = c * ri;
     const float s = __builtin_amdgcn_rcpf(__builtin_fmaf(q, q, 1.0f) * m) * (ri * f);

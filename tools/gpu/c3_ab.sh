@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/${TAG:-c3ab}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_mr.py "tests/test_gpu_configs.py::test_config3_dogstomach_literal_256_patches" -x -q --timeout 300 --timeout-method thread > $O/t.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAIL|Error|assert" $O/t.log | head; tail -5 $O/t.log; exit 1; }
+tail -1 $O/t.log
+for KN in FPM_CROP600_OLD=1 FPM_MR_XT100=1; do
+  echo "== $KN"
+  AB_ENV=$KN BENCH_ARGS="--config c3" TAG=${TAG:-c3ab}/$KN bash tools/gpu/ab_env.sh || exit 1
+done
