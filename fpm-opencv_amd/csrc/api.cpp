@@ -154,6 +154,13 @@ struct fpm_ctx {
     // replayed as a single graph launch (FPM_NO_GRAPH=1 launches them directly)
     hipGraph_t led_graph = nullptr;
     hipGraphExec_t led_graph_exec = nullptr;
+    // general path: the patches split into ngroups groups whose LED chains run
+    // on concurrent streams (forked from and joined back to the run stream), so
+    // one group's launches fill the other's partial last round of workgroups
+    int ngroups = 1;
+    static constexpr int kMaxGroups = 8;
+    hipStream_t gstream[kMaxGroups] = {};
+    hipEvent_t gfork = nullptr, gjoin[kMaxGroups] = {};
 };
 
 namespace {
@@ -179,6 +186,14 @@ void free_all(fpm_ctx *c) {
     c->allocs.clear();
     for (auto e : c->evpool) (void)hipEventDestroy(e);
     c->evpool.clear();
+    for (int g = 0; g < fpm_ctx::kMaxGroups; ++g) {
+        if (c->gstream[g]) (void)hipStreamDestroy(c->gstream[g]);
+        if (c->gjoin[g]) (void)hipEventDestroy(c->gjoin[g]);
+        c->gstream[g] = nullptr;
+        c->gjoin[g] = nullptr;
+    }
+    if (c->gfork) (void)hipEventDestroy(c->gfork);
+    c->gfork = nullptr;
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
 }
 
@@ -284,6 +299,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     st.r = r;
     st.nb = nb;
     st.B = B;
+    st.mB = B;
     st.ntx = (L + kTile - 1) / kTile;
     st.nty = st.ntx;
     st.delta1 = (float)prob->delta1;
@@ -364,6 +380,20 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
+        // patch groups on concurrent streams (FPM_PATCH_GROUPS=n overrides):
+        // two for the Np 1024 kernels, whose row launches cover a few patches
+        // in 1.3 rounds of workgroups (config 5, 8 patches: 65.5 -> 57.5 ms of
+        // LED steps per iteration; 3 or 4 groups measured slower, 79 / 77 ms)
+        const char *pg = getenv("FPM_PATCH_GROUPS");
+        c->ngroups = pg ? atoi(pg) : (reg1024 ? 2 : 1);
+        c->ngroups = std::max(1, std::min({c->ngroups, B, (int)fpm_ctx::kMaxGroups}));
+        for (int g = 1; g < c->ngroups; ++g) {
+            if (hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->gjoin[g], hipEventDisableTiming) != hipSuccess)
+                return fail(set_err(FPM_ERR_DEVICE, "patch-group stream / event creation failed"));
+        }
+        if (c->ngroups > 1 && hipEventCreateWithFlags(&c->gfork, hipEventDisableTiming) != hipSuccess)
+            return fail(set_err(FPM_ERR_DEVICE, "patch-group event creation failed"));
     } else {
         c->meas_g = c->fused_small ? np : c->fused_mr ? 10 : 16;
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
@@ -529,15 +559,41 @@ int fpm_init(fpm_ctx *c) {
 
 namespace {
 
+#define HIP_RET(x)                                   \
+    do {                                             \
+        const hipError_t e_ = (x);                   \
+        if (e_ != hipSuccess) return e_;             \
+    } while (0)
+
 hipError_t launch_general_iteration(fpm_ctx *c, hipStream_t s) {
+    // patch groups: group g = patches [g B / G, (g + 1) B / G) on stream g
+    // (group 0 on s), forked from s and joined back to it; the launches are
+    // issued LED by LED across the groups so that no group's queue runs ahead
+    const int G = c->ngroups, B = c->st.B;
+    DevState view[fpm_ctx::kMaxGroups];
+    hipStream_t gs[fpm_ctx::kMaxGroups];
+    for (int g = 0; g < G; ++g) {
+        const int b0 = g * B / G, b1 = (g + 1) * B / G;
+        view[g] = G == 1 ? c->st : patch_view(c->st, b0, b1 - b0);
+        gs[g] = g == 0 ? s : c->gstream[g];
+    }
+    if (G > 1) {
+        HIP_RET(hipEventRecord(c->gfork, s));
+        for (int g = 1; g < G; ++g) HIP_RET(hipStreamWaitEvent(gs[g], c->gfork, 0));
+    }
     for (int i = 0; i < c->prob.n_order; ++i) {
         const int led = c->order[i];
-        hipError_t e = launch_general_step(c->st, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0, s);
-        if (e != hipSuccess) return e;
+        for (int g = 0; g < G; ++g)
+            HIP_RET(launch_general_step(view[g], led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0, gs[g]));
     }
     // Np 1024: the last LED's pupil commit (the others are folded into the
     // next LED's row IDFT)
-    if (c->meas_g == c->st.np && c->st.np == 1024) return launch_pupil_commit(c->st, s);
+    if (c->meas_g == c->st.np && c->st.np == 1024)
+        for (int g = 0; g < G; ++g) HIP_RET(launch_pupil_commit(view[g], gs[g]));
+    for (int g = 1; g < G; ++g) {
+        HIP_RET(hipEventRecord(c->gjoin[g], gs[g]));
+        HIP_RET(hipStreamWaitEvent(s, c->gjoin[g], 0));
+    }
     return hipSuccess;
 }
 
@@ -578,7 +634,9 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventCreate(&e));
         c->evpool.push_back(e);
     }
-    const bool use_graph = c->path != FPM_PATH_FUSED && iters > 0 && !getenv("FPM_NO_GRAPH");
+    // patch groups launch directly: replaying the forked graph overlapped the
+    // groups less (config 5: 60.7 vs 57.5 ms per iteration of LED steps)
+    const bool use_graph = c->path != FPM_PATH_FUSED && iters > 0 && c->ngroups == 1 && !getenv("FPM_NO_GRAPH");
     if (use_graph) {
         const int r = general_graph(c);
         if (r != FPM_OK) return r;

@@ -56,6 +56,8 @@ struct DevState {
     float *pmax;      // [B][npart]
     const uint8_t *disk;  // [nb][nb] support mask
     int np, L, r, nb, B, ntx, nty;
+    int mB;           // patches per LED image in meas (= B; a patch-group view keeps the
+                      // context's count, since meas is LED-major over all patches)
     int npart;        // partial max|P| values per patch
     float delta1, delta2, eps;
     // imaginary parts of the scalars the reference adds with cv::add(UMat c2,
@@ -73,6 +75,26 @@ struct DevState {
     // column layout [led][patch][x][t][m] = I[t + g m][x] (meas_layout)
     int meas_g;
 };
+
+// patches [b0, b0 + n) of a context as a DevState of n patches (the general
+// path's patch groups, launched on concurrent streams): every per-patch array
+// is offset, meas keeps its LED-major stride mB
+inline DevState patch_view(const DevState &st, int b0, int n) {
+    DevState v = st;
+    const size_t L2 = (size_t)st.L * st.L, nb2 = (size_t)st.nb * st.nb;
+    if (v.spec) v.spec += b0 * L2;
+    if (v.spec16) v.spec16 += b0 * L2;
+    if (v.pupil) v.pupil += b0 * nb2;
+    if (v.meas) v.meas += (size_t)b0 * st.np * st.np;
+    if (v.T) v.T += (size_t)b0 * st.nb * st.np;
+    if (v.dP) v.dP += b0 * nb2;
+    if (v.tmax) v.tmax += (size_t)b0 * st.nty * st.ntx;
+    if (v.tdirty) v.tdirty += (size_t)b0 * ((st.ntx * st.nty + 31) / 32);
+    if (v.rmax) v.rmax += (size_t)b0 * st.nty;
+    if (v.pmax) v.pmax += (size_t)b0 * st.npart;
+    v.B = n;
+    return v;
+}
 
 // spectrum element i of patch b (i = y*L + x in the centred spectrum)
 __device__ __forceinline__ float2 spec_ld(const DevState &st, int b, size_t i) {

@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(256) k_colpass(DevState st, StepArgs sa, FftPl
     // amplitude replacement, fpmMain.cpp:378-393:
     //   psi = ifft2(.) (1/Np^2 scale), psi' = sqrt(I) * psi / |psi + eps| (eps on Re and Im)
     const float inv_n2 = 1.0f / ((float)np * (float)np);
-    const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
+    const uint16_t *I = st.meas + ((size_t)sa.led * st.mB + b) * np * np;
     for (int y = threadIdx.x; y < np; y += blockDim.x) {
         float2 psi = cscale(res[y], inv_n2);
         float a = sqrtf((float)I[(size_t)y * np + x]);
@@ -523,7 +523,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16
     tile_transform<true, NT, E>(tile, pl, lc, stw);
     // amplitude replacement, fpmMain.cpp:378-393 (same arithmetic as k_colpass)
     const float inv_n2 = 1.0f / ((float)np * (float)np);
-    const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
+    const uint16_t *I = st.meas + ((size_t)sa.led * st.mB + b) * np * np;
     for (int idx = threadIdx.x; idx < np * C; idx += NT) {
         const int y = idx >> lc, c = idx & cm;
         if (c >= cs) continue;
@@ -656,7 +656,7 @@ k_colpass_wave(DevState st, StepArgs sa, FftPlan pl, const float2 *__restrict__ 
     const int l = lane % LPC;
     float2 *T = st.T + (size_t)b * nb * np;
     // this lane's measurement values: rows lane + 64q of the wave's columns
-    const uint16_t *I = st.meas + ((size_t)sa.led * st.B + b) * np * np;
+    const uint16_t *I = st.meas + ((size_t)sa.led * st.mB + b) * np * np;
     uint16_t iv[NQY * CW];
 #pragma unroll
     for (int q = 0; q < NQY; ++q) {

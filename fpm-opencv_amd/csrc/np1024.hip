@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     // x0 + w: with v the unscaled IDFT value, psi = v / N^2 and
     // sqrt(I) psi / |psi + eps (1 + i)| = v / sqrt(|v + eps N^2 (1 + i)|^2 / I)
     const float nn = (float)N * (float)N, epsn = st.eps * nn, epsn_im = st.eps_im * nn;
-    const uint16_t *Ic = st.meas + (((size_t)sa.led * st.B + b) * N + x0 + w) * N + c;  // meas_layout g = Np
+    const uint16_t *Ic = st.meas + (((size_t)sa.led * st.mB + b) * N + x0 + w) * N + c;  // meas_layout g = Np
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const float iv = (float)Ic[4 * (t + 16 * j)];
