@@ -38,6 +38,11 @@ bool fused_mr_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                      const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                      unsigned long long *dbg, hipStream_t s);
+// Np 90 fused kernel (fused_s90.hip)
+bool fused_s90_supported(int np, int r, const DevState &st);
+hipError_t launch_fused_s90_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
+                                      const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
+                                      unsigned long long *dbg, hipStream_t s);
 // small-patch fused kernel (fused_small.hip, Np <= 96)
 bool fused_small_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
@@ -142,6 +147,7 @@ struct fpm_ctx {
     int *split_flags = nullptr;     //   handoff flags [KS B] + sticky abort flag + XCC ids [KS B]
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
+    bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -341,8 +347,12 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     const bool fp16 = (prob->flags & FPM_FLAG_SPEC_FP16) != 0;
     c->fused_nt = fused_threads(np, r, L, st);
     c->fused_mr = !c->fused_nt && fused_mr_supported(np, r, st);
-    c->fused_small = !c->fused_nt && !c->fused_mr && !getenv("FPM_NO_SMALL") && fused_small_supported(np, r, st);
-    const bool fused_ok = c->fused_nt || c->fused_mr || c->fused_small;
+    // Np 90 (configs 1 / 2): the register-transform kernel unless FPM_NO_S90=1
+    // selects the generic small-patch kernel
+    c->fused_s90 = !c->fused_nt && !c->fused_mr && !getenv("FPM_NO_S90") && fused_s90_supported(np, r, st);
+    c->fused_small = !c->fused_nt && !c->fused_mr && !c->fused_s90 && !getenv("FPM_NO_SMALL") &&
+                     fused_small_supported(np, r, st);
+    const bool fused_ok = c->fused_nt || c->fused_mr || c->fused_s90 || c->fused_small;
     if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_ok))
         return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
                             fp16 ? " with fp16 spectrum storage" : ""));
@@ -395,7 +405,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if (c->ngroups > 1 && hipEventCreateWithFlags(&c->gfork, hipEventDisableTiming) != hipSuccess)
             return fail(set_err(FPM_ERR_DEVICE, "patch-group event creation failed"));
     } else {
-        c->meas_g = c->fused_small ? np : c->fused_mr ? 10 : 16;
+        c->meas_g = c->fused_small ? np : c->fused_s90 ? 9 : c->fused_mr ? 10 : 16;
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
         if ((rc = dalloc(c, &c->pscr, fused_park_elems(c->fused_nt, B)))) return fail(rc);
         int n_cu = 0, coop = 0;
@@ -645,7 +655,10 @@ int fpm_run(fpm_ctx *c, int iters) {
     HIP_TRY(hipEventRecord(ev[0], c->stream));
     for (int it = 0; it < iters; ++it) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
-        if (c->path == FPM_PATH_FUSED && c->fused_small) {
+        if (c->path == FPM_PATH_FUSED && c->fused_s90) {
+            HIP_TRY(launch_fused_s90_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
+                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
+        } else if (c->path == FPM_PATH_FUSED && c->fused_small) {
             HIP_TRY(launch_fused_small_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                                  c->prob.n_order, c->tw_np, c->pl_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED && c->fused_mr) {
@@ -809,6 +822,7 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
     info->device_bytes = c->bytes;
     info->wg_per_patch = c->split_ks;
     info->fused_kernel = c->path != FPM_PATH_FUSED ? FPM_KERNEL_GENERAL
+                         : c->fused_s90        ? FPM_KERNEL_FUSED_NP90
                          : c->fused_small      ? FPM_KERNEL_FUSED_SMALL
                          : c->fused_mr         ? FPM_KERNEL_FUSED_NP200
                          : c->dist             ? FPM_KERNEL_FUSED_NP256_DIST

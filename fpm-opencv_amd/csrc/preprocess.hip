@@ -180,6 +180,7 @@ __global__ void __launch_bounds__(256) k_meas_transpose_tiles(uint16_t *meas, in
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s) {
     if (np == 256 && g == 16) return launch_layout<256, 16>(meas, nimg, fwd, s);
     if (np == 200 && g == 10) return launch_layout<200, 10>(meas, nimg, fwd, s);
+    if (np == 90 && g == 9) return launch_layout<90, 9>(meas, nimg, fwd, s);
     if (g == np && np <= 128) {
         if (nimg == 0) return hipSuccess;
         const size_t lds = (size_t)np * (np + 2) * sizeof(uint16_t);

@@ -122,6 +122,7 @@ typedef struct fpm_ctx fpm_ctx;
 #define FPM_KERNEL_FUSED_SMALL  3  /* k_fused_small (Np <= 96)                     */
 #define FPM_KERNEL_FUSED_NP256_DIST 4  /* k_fused_dist (Np 256, every phase distributed
                                           over wg_per_patch workgroups; small batches) */
+#define FPM_KERNEL_FUSED_NP90   5  /* k_fused_s90 (Np 90: register 9 x 10 transforms) */
 
 /* Which path the context runs and its per-launch geometry. */
 typedef struct fpm_info {
