@@ -50,6 +50,8 @@ HIP_SYMBOLS = (
     "fpm_get_timing", "fpm_runFPM", "fpm_last_error", "fpm_version",
     "fpm_upload_frames", "fpm_download_stack",
 )
+# test-only entry points (include/fpm_hip_debug.h)
+HIP_DEBUG_SYMBOLS = ("fpm_debug_update_coef",)
 
 
 class FpmError(RuntimeError):

@@ -19,7 +19,8 @@ def _declared(header):
     return set(re.findall(r"\b(fpm_\w+)\s*\(", text))
 
 
-@pytest.mark.parametrize("header,lib", [("fpm_hip.h", fpm_amd.HIP_LIB), ("fpm_host.h", fpm_amd.HOST_LIB)])
+@pytest.mark.parametrize("header,lib", [("fpm_hip.h", fpm_amd.HIP_LIB), ("fpm_hip_debug.h", fpm_amd.HIP_LIB),
+                                        ("fpm_host.h", fpm_amd.HOST_LIB)])
 def test_library_exports_every_declared_symbol(header, lib):
     names = _declared(header)
     assert names, header
@@ -30,6 +31,7 @@ def test_library_exports_every_declared_symbol(header, lib):
 
 def test_python_mirror_covers_header():
     assert _declared("fpm_hip.h") == set(fpm_amd.HIP_SYMBOLS)
+    assert _declared("fpm_hip_debug.h") == set(fpm_amd.HIP_DEBUG_SYMBOLS)
     assert _declared("fpm_host.h") == set(host.HOST_SYMBOLS)
 
 
@@ -60,3 +62,8 @@ def test_flag_and_path_constants_match_header():
     assert int(defs["FPM_FLAG_SPEC_FP16"]) == fpm_amd.FLAG_SPEC_FP16
     assert (int(defs["FPM_PATH_AUTO"]), int(defs["FPM_PATH_GENERAL"]), int(defs["FPM_PATH_FUSED"])) == \
         (fpm_amd.PATH_AUTO, fpm_amd.PATH_GENERAL, fpm_amd.PATH_FUSED)
+    kern = dict(re.findall(r"#define\s+FPM_KERNEL_(\w+)\s+(\d+)", text))
+    assert {k: int(v) for k, v in kern.items()} == {
+        "GENERAL": fpm_amd.KERNEL_GENERAL, "FUSED_NP256": fpm_amd.KERNEL_FUSED_NP256,
+        "FUSED_NP200": fpm_amd.KERNEL_FUSED_NP200, "FUSED_SMALL": fpm_amd.KERNEL_FUSED_SMALL,
+        "FUSED_NP256_DIST": fpm_amd.KERNEL_FUSED_NP256_DIST, "FUSED_NP90": fpm_amd.KERNEL_FUSED_NP90}
