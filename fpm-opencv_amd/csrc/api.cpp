@@ -158,13 +158,14 @@ struct fpm_ctx {
     fpm_timing timing{};
     // general path: one iteration's 4*n_order launches captured once and
     // replayed as a single graph launch (FPM_NO_GRAPH=1 launches them directly)
-    hipGraph_t led_graph = nullptr;
-    hipGraphExec_t led_graph_exec = nullptr;
     // general path: the patches split into ngroups groups whose LED chains run
     // on concurrent streams (forked from and joined back to the run stream), so
-    // one group's launches fill the other's partial last round of workgroups
+    // one group's launches fill the other's partial last round of workgroups;
+    // one captured graph per group
     int ngroups = 1;
     static constexpr int kMaxGroups = 8;
+    hipGraph_t led_graph[kMaxGroups] = {};
+    hipGraphExec_t led_graph_exec[kMaxGroups] = {};
     hipStream_t gstream[kMaxGroups] = {};
     hipEvent_t gfork = nullptr, gjoin[kMaxGroups] = {};
 };
@@ -184,10 +185,12 @@ int dalloc(fpm_ctx *c, T **p, size_t count) {
 }
 
 void free_all(fpm_ctx *c) {
-    if (c->led_graph_exec) (void)hipGraphExecDestroy(c->led_graph_exec);
-    if (c->led_graph) (void)hipGraphDestroy(c->led_graph);
-    c->led_graph_exec = nullptr;
-    c->led_graph = nullptr;
+    for (int g = 0; g < fpm_ctx::kMaxGroups; ++g) {
+        if (c->led_graph_exec[g]) (void)hipGraphExecDestroy(c->led_graph_exec[g]);
+        if (c->led_graph[g]) (void)hipGraphDestroy(c->led_graph[g]);
+        c->led_graph_exec[g] = nullptr;
+        c->led_graph[g] = nullptr;
+    }
     for (void *p : c->allocs) (void)hipFree(p);
     c->allocs.clear();
     for (auto e : c->evpool) (void)hipEventDestroy(e);
@@ -575,57 +578,94 @@ namespace {
         if (e_ != hipSuccess) return e_;             \
     } while (0)
 
-hipError_t launch_general_iteration(fpm_ctx *c, hipStream_t s) {
-    // patch groups: group g = patches [g B / G, (g + 1) B / G) on stream g
-    // (group 0 on s), forked from s and joined back to it; the launches are
-    // issued LED by LED across the groups so that no group's queue runs ahead
+// patch group g = patches [g B / G, (g + 1) B / G)
+DevState group_view(const fpm_ctx *c, int g) {
     const int G = c->ngroups, B = c->st.B;
-    DevState view[fpm_ctx::kMaxGroups];
-    hipStream_t gs[fpm_ctx::kMaxGroups];
-    for (int g = 0; g < G; ++g) {
-        const int b0 = g * B / G, b1 = (g + 1) * B / G;
-        view[g] = G == 1 ? c->st : patch_view(c->st, b0, b1 - b0);
-        gs[g] = g == 0 ? s : c->gstream[g];
-    }
-    if (G > 1) {
-        HIP_RET(hipEventRecord(c->gfork, s));
-        for (int g = 1; g < G; ++g) HIP_RET(hipStreamWaitEvent(gs[g], c->gfork, 0));
-    }
+    return G == 1 ? c->st : patch_view(c->st, g * B / G, (g + 1) * B / G - g * B / G);
+}
+
+// one group's LED chain of an iteration on stream s
+hipError_t launch_group_chain(const fpm_ctx *c, const DevState &v, hipStream_t s) {
     for (int i = 0; i < c->prob.n_order; ++i) {
         const int led = c->order[i];
-        for (int g = 0; g < G; ++g)
-            HIP_RET(launch_general_step(view[g], led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0, gs[g]));
+        HIP_RET(launch_general_step(v, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0, s));
     }
     // Np 1024: the last LED's pupil commit (the others are folded into the
     // next LED's row IDFT)
-    if (c->meas_g == c->st.np && c->st.np == 1024)
-        for (int g = 0; g < G; ++g) HIP_RET(launch_pupil_commit(view[g], gs[g]));
-    for (int g = 1; g < G; ++g) {
-        HIP_RET(hipEventRecord(c->gjoin[g], gs[g]));
+    if (c->meas_g == c->st.np && c->st.np == 1024) HIP_RET(launch_pupil_commit(v, s));
+    return hipSuccess;
+}
+
+// stream of group g when the run stream is s (group 0 runs on s itself)
+hipStream_t group_stream(const fpm_ctx *c, int g, hipStream_t s) { return g == 0 ? s : c->gstream[g]; }
+
+// fork the group streams from s / join them back to s
+hipError_t fork_groups(fpm_ctx *c, hipStream_t s) {
+    if (c->ngroups < 2) return hipSuccess;
+    HIP_RET(hipEventRecord(c->gfork, s));
+    for (int g = 1; g < c->ngroups; ++g) HIP_RET(hipStreamWaitEvent(c->gstream[g], c->gfork, 0));
+    return hipSuccess;
+}
+hipError_t join_groups(fpm_ctx *c, hipStream_t s) {
+    for (int g = 1; g < c->ngroups; ++g) {
+        HIP_RET(hipEventRecord(c->gjoin[g], c->gstream[g]));
         HIP_RET(hipStreamWaitEvent(s, c->gjoin[g], 0));
     }
     return hipSuccess;
 }
 
-// The general path issues four launches per LED (~1200 per iteration at 293
-// LEDs); every argument is fixed once the context exists, so one iteration is
-// captured on the context's own stream and replayed on c->stream.
-int general_graph(fpm_ctx *c) {
-    if (c->led_graph_exec) return FPM_OK;
-    hipStream_t cs = c->own_stream;
-    HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    hipError_t e = launch_general_iteration(c, cs);
-    hipGraph_t g = nullptr;
-    hipError_t e2 = hipStreamEndCapture(cs, &g);
-    if (e == hipSuccess) e = e2;
-    if (e == hipSuccess) e = hipGraphInstantiate(&c->led_graph_exec, g, nullptr, nullptr, 0);
-    if (e != hipSuccess) {
-        if (g) (void)hipGraphDestroy(g);
-        c->led_graph_exec = nullptr;
-        return set_err(FPM_ERR_DEVICE, "general-path graph capture: %s", hipGetErrorString(e));
+// direct launches (FPM_NO_GRAPH=1): issued LED by LED across the groups so
+// that no group's queue runs ahead
+hipError_t launch_general_iteration(fpm_ctx *c, hipStream_t s) {
+    const int G = c->ngroups;
+    DevState view[fpm_ctx::kMaxGroups];
+    for (int g = 0; g < G; ++g) view[g] = group_view(c, g);
+    HIP_RET(fork_groups(c, s));
+    for (int i = 0; i < c->prob.n_order; ++i) {
+        const int led = c->order[i];
+        for (int g = 0; g < G; ++g)
+            HIP_RET(launch_general_step(view[g], led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0,
+                                        group_stream(c, g, s)));
     }
-    c->led_graph = g;
+    if (c->meas_g == c->st.np && c->st.np == 1024)
+        for (int g = 0; g < G; ++g) HIP_RET(launch_pupil_commit(view[g], group_stream(c, g, s)));
+    return join_groups(c, s);
+}
+
+// The general path issues four launches per LED (~1200 per iteration at 293
+// LEDs); every argument is fixed once the context exists, so each group's
+// chain of one iteration is captured once (on its own stream) and replayed:
+// one graph launch per group per iteration, the groups' graphs on forked streams.
+int general_graph(fpm_ctx *c) {
+    if (c->led_graph_exec[0]) return FPM_OK;
+    for (int g = 0; g < c->ngroups; ++g) {
+        hipStream_t cs = group_stream(c, g, c->own_stream);
+        HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        hipError_t e = launch_group_chain(c, group_view(c, g), cs);
+        hipGraph_t gr = nullptr;
+        hipError_t e2 = hipStreamEndCapture(cs, &gr);
+        if (e == hipSuccess) e = e2;
+        if (e == hipSuccess) e = hipGraphInstantiate(&c->led_graph_exec[g], gr, nullptr, nullptr, 0);
+        if (e != hipSuccess) {
+            if (gr) (void)hipGraphDestroy(gr);
+            c->led_graph_exec[g] = nullptr;
+            for (int h = 0; h < g; ++h) {
+                (void)hipGraphExecDestroy(c->led_graph_exec[h]);
+                (void)hipGraphDestroy(c->led_graph[h]);
+                c->led_graph_exec[h] = nullptr;
+                c->led_graph[h] = nullptr;
+            }
+            return set_err(FPM_ERR_DEVICE, "general-path graph capture: %s", hipGetErrorString(e));
+        }
+        c->led_graph[g] = gr;
+    }
     return FPM_OK;
+}
+
+hipError_t launch_general_graphs(fpm_ctx *c, hipStream_t s) {
+    HIP_RET(fork_groups(c, s));
+    for (int g = 0; g < c->ngroups; ++g) HIP_RET(hipGraphLaunch(c->led_graph_exec[g], group_stream(c, g, s)));
+    return join_groups(c, s);
 }
 
 }  // namespace
@@ -644,9 +684,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventCreate(&e));
         c->evpool.push_back(e);
     }
-    // patch groups launch directly: replaying the forked graph overlapped the
-    // groups less (config 5: 60.7 vs 57.5 ms per iteration of LED steps)
-    const bool use_graph = c->path != FPM_PATH_FUSED && iters > 0 && c->ngroups == 1 && !getenv("FPM_NO_GRAPH");
+    const bool use_graph = c->path != FPM_PATH_FUSED && iters > 0 && !getenv("FPM_NO_GRAPH");
     if (use_graph) {
         const int r = general_graph(c);
         if (r != FPM_OK) return r;
@@ -672,7 +710,7 @@ int fpm_run(fpm_ctx *c, int iters) {
                                            c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->split_ks,
                                            c->dbg, c->xch, c->split_flags, c->stream));
         } else if (use_graph) {
-            HIP_TRY(hipGraphLaunch(c->led_graph_exec, c->stream));
+            HIP_TRY(launch_general_graphs(c, c->stream));
         } else {
             HIP_TRY(launch_general_iteration(c, c->stream));
         }
