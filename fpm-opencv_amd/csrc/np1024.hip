@@ -8,7 +8,7 @@
 // unchanged:
 //   R1 k_rows1024_inv   a wave per support-box row: gather O*P on the disk,
 //                       row IDFT, T row stored as 128-byte segments
-//   C  k_cols1024       a block per 4 adjacent columns (a wave each): box rows
+//   C  k_cols1024       a block per 8 adjacent columns (a wave each): box rows
 //                       of T staged through an LDS strip, column IDFT,
 //                       amplitude replacement against the stack read
 //                       column-major (meas_layout g = Np), column DFT, box rows
@@ -39,6 +39,7 @@
 #include "fpm_state.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace fpm {
 
@@ -52,7 +53,6 @@ constexpr int CXP = 17;            // cross-group exchange row pitch (complex)
 // 4 x 8 x CXP tile in the same space.  Half tiles: 4.6 KB per wave instead of
 // 18 KB, so R1/R2 fit six blocks per CU instead of three.
 constexpr int WTILE = 4 * XTILE_H;
-constexpr int SPC = WPB + 1;       // column-pass strip pitch (complex)
 static_assert(4 * 8 * CXP <= WTILE, "cross-group tile");
 }  // namespace n1k
 
@@ -144,7 +144,7 @@ __device__ __forceinline__ int fold(int k) { return k < n1k::H ? k : k - n1k::N;
 
 // stage the N-point twiddle table; returns the table
 __device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__restrict__ tw) {
-    for (int i = threadIdx.x; i < n1k::N; i += n1k::NT) sm[i] = tw[i];
+    for (int i = threadIdx.x; i < n1k::N; i += blockDim.x) sm[i] = tw[i];
     __syncthreads();
     return sm;
 }
@@ -215,25 +215,28 @@ __global__ void __launch_bounds__(n1k::NT) FPM_N1K_ROWS_OCC k_rows1024_inv(DevSt
         for (int bb = 0; bb < 4; ++bb) T[16 * bb + 256 * p] = x[4 * p + bb];
 }
 
-// C: grid (N / WPB, B), block NT
-__global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4))) k_cols1024(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+// C: grid (N / CW, B), block 64 CW: CW adjacent columns, a wave each (CW 8:
+// 64-byte row segments of T per block, the default; 4 / 16 by FPM_N1K_CW)
+template <int CW>
+__global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4))) k_cols1024(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n1k;
+    constexpr int NTC = 64 * CW, SPCC = CW + 1;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const float2 *twL = stage_twiddles(sm, tw);
-    float2 *strip = sm + N;            // nb x SPC (box rows only); the wave tiles
+    float2 *strip = sm + N;            // nb x SPCC (box rows only); the wave tiles
     float2 *wt = strip + w * WTILE;    // alias it while every column is in registers
     // XCD-aware column groups: the dispatcher deals blocks round-robin over the
     // 8 XCDs, so XCD k gets column groups k*G/8 .. (k+1)*G/8 - 1 (contiguous)
-    constexpr int G = N / WPB;
+    constexpr int G = N / CW;
     const int cg = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);
-    const int r = st.r, nb = st.nb, b = blockIdx.y, x0 = cg * WPB;
+    const int r = st.r, nb = st.nb, b = blockIdx.y, x0 = cg * CW;
     float2 *T = st.T + (size_t)b * nb * N + x0;
     // FFT row i of a column is box row j = i + r (i <= r) or i - N + r
     // (i >= N - r) (:364: every other row is zero)
-    for (int idx = threadIdx.x; idx < nb * WPB; idx += NT) {
-        const int j = idx / WPB, cc = idx - j * WPB;
-        strip[j * SPC + cc] = T[(size_t)j * N + cc];
+    for (int idx = threadIdx.x; idx < nb * CW; idx += NTC) {
+        const int j = idx / CW, cc = idx - j * CW;
+        strip[j * SPCC + cc] = T[(size_t)j * N + cc];
     }
     __syncthreads();
     auto boxrow = [&](int i) { return i <= r ? i + r : (i >= N - r ? i - N + r : -1); };
@@ -243,7 +246,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int j = boxrow(t + 16 * (4 * c + bb) + 256 * p);
-            x[4 * p + bb] = j >= 0 ? strip[j * SPC + w] : make_float2(0.f, 0.f);
+            x[4 * p + bb] = j >= 0 ? strip[j * SPCC + w] : make_float2(0.f, 0.f);
         }
     __syncthreads();
     w1k_ND<true>(x, wt, twL, c, t, xrd);                                 // :365 (columns)
@@ -267,12 +270,12 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int j = boxrow(t + 16 * (4 * c + bb) + 256 * p);
-            if (j >= 0) strip[j * SPC + w] = x[4 * p + bb];
+            if (j >= 0) strip[j * SPCC + w] = x[4 * p + bb];
         }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < nb * WPB; idx += NT) {
-        const int j = idx / WPB, cc = idx - j * WPB;
-        T[(size_t)j * N + cc] = strip[j * SPC + cc];
+    for (int idx = threadIdx.x; idx < nb * CW; idx += NTC) {
+        const int j = idx / CW, cc = idx - j * CW;
+        T[(size_t)j * N + cc] = strip[j * SPCC + cc];
     }
 }
 
@@ -328,13 +331,26 @@ hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const
     using namespace n1k;
     if (!np1024_supported(st.np, st.r) || st.meas_g != N || st.npart < st.nb) return hipErrorInvalidValue;
     const size_t lds_r = (size_t)(N + WPB * WTILE) * sizeof(float2);
-    const size_t strip = std::max((size_t)st.nb * SPC, (size_t)WPB * WTILE);
+    // column-pass width: 8 columns per block (64-byte row segments of T;
+    // config 5: 56.5-57.4 vs 58.3-59.1 ms of LED steps with 4), FPM_N1K_CW=4/16
+    const char *cwe = std::getenv("FPM_N1K_CW");
+    const int cwv = cwe ? std::atoi(cwe) : 8;
+    const int cw = cwv == 4 || cwv == 16 ? cwv : 8;
+    const size_t strip = std::max((size_t)st.nb * (cw + 1), (size_t)cw * WTILE);
     const size_t lds_c = (N + strip) * sizeof(float2);
-    hipError_t e = hipFuncSetAttribute((const void *)k_cols1024, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
+    const void *fc = cw == 16 ? (const void *)k_cols1024<16>
+                     : cw == 8 ? (const void *)k_cols1024<8>
+                               : (const void *)k_cols1024<4>;
+    hipError_t e = hipFuncSetAttribute(fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
     if (e != hipSuccess) return e;
     const dim3 rgrid((st.nb + WPB - 1) / WPB, st.B);
     hipLaunchKernelGGL(k_rows1024_inv, rgrid, dim3(NT), lds_r, s, st, sa, tw, commit ? 1 : 0);
-    hipLaunchKernelGGL(k_cols1024, dim3(N / WPB, st.B), dim3(NT), lds_c, s, st, sa, tw);
+    if (cw == 16)
+        hipLaunchKernelGGL(k_cols1024<16>, dim3(N / 16, st.B), dim3(1024), lds_c, s, st, sa, tw);
+    else if (cw == 8)
+        hipLaunchKernelGGL(k_cols1024<8>, dim3(N / 8, st.B), dim3(512), lds_c, s, st, sa, tw);
+    else
+        hipLaunchKernelGGL(k_cols1024<4>, dim3(N / 4, st.B), dim3(256), lds_c, s, st, sa, tw);
     hipLaunchKernelGGL(k_rows1024_fwd, rgrid, dim3(NT), lds_r, s, st, sa, tw);
     return hipGetLastError();
 }
