@@ -191,8 +191,14 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             for (int k = 0; k < 20; ++k) row[10 * k] = v[k];
         }
         if (tid == 0) *ccnt = NW;  // pass-B block counter (blocks 0..NW-1 are preassigned)
-        __syncthreads();  // T complete
+        __syncthreads();  // T complete; the previous LED's max|P| partials
         FPM_STAMP(7)
+        if (it > 0) {  // max|P| of the previous pupil update (:415)
+            float pm2 = red[32];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
+            pm = sqrtf(pm2);
+        }
 
         // ---- B: IDFT, amplitude replacement, DFT per column (:365-394).  Column
         // blocks of GPW: block c gives group gw of a wave column GPW c + gw; wave w
@@ -253,7 +259,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
         }
-        __syncthreads();  // T rows are reused for the pupil numerator below
+        // no barrier: a group reads and rewrites only its own T row g in C and
+        // in the update below
         FPM_STAMP(8)
 
         // ---- object update on the support (:405-447) and pupil numerator
@@ -350,16 +357,23 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
                 pmx = fmaxf(pmx, cabs2(P[s]));
             }
         }
+        // max|P| partials per wave, folded after the next LED's A barrier (the
+        // next update is the first use): this phase needs no barrier
         pmx = wave_max(pmx);
         if (lane == 0) red[32 + w] = pmx;
-        __syncthreads();
-        float pm2 = red[32];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
-        pm = sqrtf(pm2);
         FPM_STAMP(6)
     }
 #undef FPM_STAMP
+    auto fold_pm = [&]() {
+        float pm2 = red[32];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
+        return sqrtf(pm2);
+    };
+    if (a.n_order > 0) {
+        __syncthreads();  // the last LED's red[32..]
+        pm = fold_pm();
+    }
     // stamps of the first and the last wave (the barrier waits show who is slow)
     if (a.dbg && (tid == 0 || tid == NT - 64))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
