@@ -81,6 +81,59 @@ __device__ __forceinline__ pf2 pmulc(pf2 a, pf2 w) {
     return d;
 }
 
+// Twiddle multiplies of a 16-register column, py[m] *= w[m] (CONJ: by
+// conj(w[m])) for m = 1..15, in three asm blocks of five: the five partial
+// products first, then the five fmas, so no VOP3P read directly follows the
+// VALU write it depends on.  With one pmul / pmulc per asm fma the compiler
+// places each fma right after its mul and pays the hazard's wait state as an
+// `s_nop 0` per twiddle (it cannot see into the asm, so it also pads the
+// boundary of every block: fewer, larger blocks).
+//   pmulc: t = a * w.xx, a = a.yx * (w.y, -w.y) + t
+//   pmul:  t = a.xx * w, a = a.yy * (-w.y, w.x) + t
+template <bool CONJ>
+__device__ __forceinline__ void ptw5(pf2 &a0, pf2 &a1, pf2 &a2, pf2 &a3, pf2 &a4, pf2 w0, pf2 w1, pf2 w2, pf2 w3,
+                                     pf2 w4) {
+    pf2 t0, t1, t2, t3, t4;
+    if constexpr (CONJ)
+        asm("v_pk_mul_f32 %0, %5, %10 op_sel_hi:[1,0]\n\t"
+            "v_pk_mul_f32 %1, %6, %11 op_sel_hi:[1,0]\n\t"
+            "v_pk_mul_f32 %2, %7, %12 op_sel_hi:[1,0]\n\t"
+            "v_pk_mul_f32 %3, %8, %13 op_sel_hi:[1,0]\n\t"
+            "v_pk_mul_f32 %4, %9, %14 op_sel_hi:[1,0]\n\t"
+            "v_pk_fma_f32 %5, %5, %10, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
+            "v_pk_fma_f32 %6, %6, %11, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
+            "v_pk_fma_f32 %7, %7, %12, %2 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
+            "v_pk_fma_f32 %8, %8, %13, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
+            "v_pk_fma_f32 %9, %9, %14, %4 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
+            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4)
+            : "v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
+    else
+        asm("v_pk_mul_f32 %0, %5, %10 op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %1, %6, %11 op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %2, %7, %12 op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %3, %8, %13 op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %4, %9, %14 op_sel_hi:[0,1]\n\t"
+            "v_pk_fma_f32 %5, %5, %10, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+            "v_pk_fma_f32 %6, %6, %11, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+            "v_pk_fma_f32 %7, %7, %12, %2 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+            "v_pk_fma_f32 %8, %8, %13, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+            "v_pk_fma_f32 %9, %9, %14, %4 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4)
+            : "v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
+}
+template <bool CONJ, class TW>
+__device__ __forceinline__ void ptwiddle15(pf2 (&py)[16], const TW &wt) {
+#ifndef FPM_TW_SINGLE  // A/B: one asm fma per twiddle (round 2)
+#pragma unroll
+    for (int m = 1; m < 16; m += 5)
+        ptw5<CONJ>(py[m], py[m + 1], py[m + 2], py[m + 3], py[m + 4], pin(wt[m]), pin(wt[m + 1]), pin(wt[m + 2]),
+                   pin(wt[m + 3]), pin(wt[m + 4]));
+#else
+#pragma unroll
+    for (int m = 1; m < 16; ++m) py[m] = CONJ ? pmulc(py[m], pin(wt[m])) : pmul(py[m], pin(wt[m]));
+#endif
+}
+
 // radix-4 butterfly in place (the scalar dft4 of fft_lds.hpp, packed)
 template <bool INV>
 __device__ __forceinline__ void pbf4(pf2 &a0, pf2 &a1, pf2 &a2, pf2 &a3) {

@@ -187,8 +187,7 @@ __device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], fl
     pf2 pv[16], py[16];
     to_pk(v, pv);
     pdft16_in6<true>(pv, py);
-#pragma unroll
-    for (int m1 = 1; m1 < 16; ++m1) py[m1] = pmulc(py[m1], pin(wt[m1]));
+    ptwiddle15<true>(py, wt);
     float2 y[16];
     from_pk(py, y);
     xchg<HALF>(scr, t, xrd, y, v);
@@ -204,8 +203,7 @@ __device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], flo
     pf2 pv[16], py[16], po[6];
     to_pk(v, pv);
     pdft16<false>(pv, py);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) py[k1] = pmul(py[k1], pin(wt[k1]));
+    ptwiddle15<false>(py, wt);
     float2 y[16];
     from_pk(py, y);
     xchg<HALF>(scr, t, xrd, y, v);
@@ -222,8 +220,7 @@ __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[
     pf2 pv[16], py[16], po[6];
     to_pk(v, pv);
     pdft16_inhalf<false, H>(pv, py);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) py[k1] = pmul(py[k1], pin(wt[k1]));
+    ptwiddle15<false>(py, wt);
     float2 y[16];
     from_pk(py, y);
     xchg<HALF>(scr, t, xrd, y, v);
@@ -244,8 +241,7 @@ __device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[
         pf2 pv[16], py[16], po[6];
         to_pk(v, pv);
         pdft16_inquarter<false, P>(pv, py);
-#pragma unroll
-        for (int k1 = 1; k1 < 16; ++k1) py[k1] = pmul(py[k1], pin(wt[k1]));
+        ptwiddle15<false>(py, wt);
         float2 y[16];
         from_pk(py, y);
         xchg<HALF>(scr, t, xrd, y, v);
