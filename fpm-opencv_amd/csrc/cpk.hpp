@@ -90,44 +90,76 @@ __device__ __forceinline__ pf2 pmulc(pf2 a, pf2 w) {
 // boundary of every block: fewer, larger blocks).
 //   pmulc: t = a * w.xx, a = a.yx * (w.y, -w.y) + t
 //   pmul:  t = a.xx * w, a = a.yy * (-w.y, w.x) + t
-template <bool CONJ>
-__device__ __forceinline__ void ptw5(pf2 &a0, pf2 &a1, pf2 &a2, pf2 &a3, pf2 &a4, pf2 w0, pf2 w1, pf2 w2, pf2 w3,
-                                     pf2 w4) {
-    pf2 t0, t1, t2, t3, t4;
-    if constexpr (CONJ)
-        asm("v_pk_mul_f32 %0, %5, %10 op_sel_hi:[1,0]\n\t"
-            "v_pk_mul_f32 %1, %6, %11 op_sel_hi:[1,0]\n\t"
-            "v_pk_mul_f32 %2, %7, %12 op_sel_hi:[1,0]\n\t"
-            "v_pk_mul_f32 %3, %8, %13 op_sel_hi:[1,0]\n\t"
-            "v_pk_mul_f32 %4, %9, %14 op_sel_hi:[1,0]\n\t"
-            "v_pk_fma_f32 %5, %5, %10, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
-            "v_pk_fma_f32 %6, %6, %11, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
-            "v_pk_fma_f32 %7, %7, %12, %2 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
-            "v_pk_fma_f32 %8, %8, %13, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
-            "v_pk_fma_f32 %9, %9, %14, %4 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
-            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4)
-            : "v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
-    else
-        asm("v_pk_mul_f32 %0, %5, %10 op_sel_hi:[0,1]\n\t"
-            "v_pk_mul_f32 %1, %6, %11 op_sel_hi:[0,1]\n\t"
-            "v_pk_mul_f32 %2, %7, %12 op_sel_hi:[0,1]\n\t"
-            "v_pk_mul_f32 %3, %8, %13 op_sel_hi:[0,1]\n\t"
-            "v_pk_mul_f32 %4, %9, %14 op_sel_hi:[0,1]\n\t"
-            "v_pk_fma_f32 %5, %5, %10, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
-            "v_pk_fma_f32 %6, %6, %11, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
-            "v_pk_fma_f32 %7, %7, %12, %2 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
-            "v_pk_fma_f32 %8, %8, %13, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
-            "v_pk_fma_f32 %9, %9, %14, %4 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4)
-            : "v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
+// one partial product / one fma of a twiddle multiply in asm text (operand
+// numbers are literal tokens); C: conjugate twiddle (pmulc), F: pmul
+#define FPM_TWMUL_C(t, a, w) "v_pk_mul_f32 %" #t ", %" #a ", %" #w " op_sel_hi:[1,0]\n\t"
+#define FPM_TWFMA_C(a, w, t) "v_pk_fma_f32 %" #a ", %" #a ", %" #w ", %" #t " op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]\n\t"
+#define FPM_TWMUL_F(t, a, w) "v_pk_mul_f32 %" #t ", %" #a ", %" #w " op_sel_hi:[0,1]\n\t"
+#define FPM_TWFMA_F(a, w, t) "v_pk_fma_f32 %" #a ", %" #a ", %" #w ", %" #t " op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+// blocks of N = 2 .. 5 twiddles: operands t0..t(N-1), a0..a(N-1), w0..w(N-1)
+#define FPM_TW2(K) FPM_TWMUL_##K(0, 2, 4) FPM_TWMUL_##K(1, 3, 5) FPM_TWFMA_##K(2, 4, 0) FPM_TWFMA_##K(3, 5, 1)
+#define FPM_TW3(K) FPM_TWMUL_##K(0, 3, 6) FPM_TWMUL_##K(1, 4, 7) FPM_TWMUL_##K(2, 5, 8) \
+    FPM_TWFMA_##K(3, 6, 0) FPM_TWFMA_##K(4, 7, 1) FPM_TWFMA_##K(5, 8, 2)
+#define FPM_TW4(K) FPM_TWMUL_##K(0, 4, 8) FPM_TWMUL_##K(1, 5, 9) FPM_TWMUL_##K(2, 6, 10) FPM_TWMUL_##K(3, 7, 11) \
+    FPM_TWFMA_##K(4, 8, 0) FPM_TWFMA_##K(5, 9, 1) FPM_TWFMA_##K(6, 10, 2) FPM_TWFMA_##K(7, 11, 3)
+#define FPM_TW5(K) FPM_TWMUL_##K(0, 5, 10) FPM_TWMUL_##K(1, 6, 11) FPM_TWMUL_##K(2, 7, 12) FPM_TWMUL_##K(3, 8, 13) \
+    FPM_TWMUL_##K(4, 9, 14) FPM_TWFMA_##K(5, 10, 0) FPM_TWFMA_##K(6, 11, 1) FPM_TWFMA_##K(7, 12, 2)                \
+    FPM_TWFMA_##K(8, 13, 3) FPM_TWFMA_##K(9, 14, 4)
+// a[i] *= w[i] (CONJ: conj(w[i])) for i < N, N = 2..5, in one asm block
+template <bool CONJ, int N>
+__device__ __forceinline__ void ptw_block(pf2 *a, const pf2 *w) {
+    static_assert(N >= 2 && N <= 5, "block of 2..5 twiddles");
+    pf2 t[N];
+    if constexpr (N == 2) {
+        if constexpr (CONJ)
+            asm(FPM_TW2(C) : "=&v"(t[0]), "=&v"(t[1]), "+v"(a[0]), "+v"(a[1]) : "v"(w[0]), "v"(w[1]));
+        else
+            asm(FPM_TW2(F) : "=&v"(t[0]), "=&v"(t[1]), "+v"(a[0]), "+v"(a[1]) : "v"(w[0]), "v"(w[1]));
+    } else if constexpr (N == 3) {
+        if constexpr (CONJ)
+            asm(FPM_TW3(C) : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "+v"(a[0]), "+v"(a[1]), "+v"(a[2])
+                : "v"(w[0]), "v"(w[1]), "v"(w[2]));
+        else
+            asm(FPM_TW3(F) : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "+v"(a[0]), "+v"(a[1]), "+v"(a[2])
+                : "v"(w[0]), "v"(w[1]), "v"(w[2]));
+    } else if constexpr (N == 4) {
+        if constexpr (CONJ)
+            asm(FPM_TW4(C) : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
+                "+v"(a[3]) : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+        else
+            asm(FPM_TW4(F) : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
+                "+v"(a[3]) : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+    } else {
+        if constexpr (CONJ)
+            asm(FPM_TW5(C) : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "+v"(a[0]), "+v"(a[1]),
+                "+v"(a[2]), "+v"(a[3]), "+v"(a[4]) : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]));
+        else
+            asm(FPM_TW5(F) : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "+v"(a[0]), "+v"(a[1]),
+                "+v"(a[2]), "+v"(a[3]), "+v"(a[4]) : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]));
+    }
+}
+// a[i] *= w[i] for i in [1, M) (a[0] has no twiddle) in blocks of 3..5
+template <bool CONJ, int M>
+__device__ __forceinline__ void ptw_range(pf2 (&a)[M > 0 ? M : 1], const pf2 (&w)[M > 0 ? M : 1]) {
+    constexpr int n = M - 1;                          // twiddles
+    constexpr int nb = (n + 4) / 5;                   // blocks
+#pragma unroll
+    for (int b = 0, i = 1; b < nb; ++b) {
+        const int len = (n - (i - 1)) / (nb - b);     // spread evenly: every block 3..5
+        if (len == 5) ptw_block<CONJ, 5>(&a[i], &w[i]);
+        else if (len == 4) ptw_block<CONJ, 4>(&a[i], &w[i]);
+        else ptw_block<CONJ, 3>(&a[i], &w[i]);
+        i += len;
+    }
 }
 template <bool CONJ, class TW>
 __device__ __forceinline__ void ptwiddle15(pf2 (&py)[16], const TW &wt) {
 #ifndef FPM_TW_SINGLE  // A/B: one asm fma per twiddle (round 2)
+    pf2 w[16];
 #pragma unroll
-    for (int m = 1; m < 16; m += 5)
-        ptw5<CONJ>(py[m], py[m + 1], py[m + 2], py[m + 3], py[m + 4], pin(wt[m]), pin(wt[m + 1]), pin(wt[m + 2]),
-                   pin(wt[m + 3]), pin(wt[m + 4]));
+    for (int m = 1; m < 16; ++m) w[m] = pin(wt[m]);
+    w[0] = w[1];
+    ptw_range<CONJ, 16>(py, w);
 #else
 #pragma unroll
     for (int m = 1; m < 16; ++m) py[m] = CONJ ? pmulc(py[m], pin(wt[m])) : pmul(py[m], pin(wt[m]));
@@ -177,6 +209,7 @@ __device__ __forceinline__ pf2 pw16(pf2 a) {
 // position k1 + 4 m1 *= W16^{k1 m1}; position 10 (W16^4) is left to pbf4_w2
 template <bool INV>
 __device__ __forceinline__ void pmid_tw(pf2 (&v)[16]) {
+#ifdef FPM_MID_SERIAL  // A/B: one twiddle after the other (round 2)
     v[5] = pw16<INV, 1>(v[5]);
     v[6] = pw16<INV, 2>(v[6]);
     v[7] = pw16<INV, 3>(v[7]);
@@ -185,6 +218,37 @@ __device__ __forceinline__ void pmid_tw(pf2 (&v)[16]) {
     v[13] = pw16<INV, 3>(v[13]);
     v[14] = pw16<INV, 6>(v[14]);
     v[15] = pw16<INV, 9>(v[15]);
+#else
+    // the same operations, first steps of all eight twiddles before the
+    // second steps (no VOP3P read right after the write it depends on; the
+    // four W4 rotations in one asm block: no padding between blocks)
+    constexpr float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f, R2 = 0.70710678118654752440f;
+    constexpr float s1 = INV ? -S1 : S1, s3 = INV ? -C1 : C1;  // J = 1: (C1, S1); J = 3: (S1, C1); J = 9: -(C1, S1)
+    const pf2 t5 = v[5] * C1, t7 = v[7] * S1, t13 = v[13] * S1, t15 = v[15] * (-C1);
+    pf2 u6, u9, u11, u14;  // (1 -+ i) a for J = 2, (1 +- i) a for J = 6
+    if constexpr (INV)
+        asm("v_pk_add_f32 %0, %4, %4 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]\n\t"
+            "v_pk_add_f32 %1, %5, %5 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]\n\t"
+            "v_pk_add_f32 %2, %6, %6 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]\n\t"
+            "v_pk_add_f32 %3, %7, %7 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]"
+            : "=&v"(u6), "=&v"(u9), "=&v"(u11), "=v"(u14)
+            : "v"(v[6]), "v"(v[9]), "v"(v[11]), "v"(v[14]));
+    else
+        asm("v_pk_add_f32 %0, %4, %4 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]\n\t"
+            "v_pk_add_f32 %1, %5, %5 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]\n\t"
+            "v_pk_add_f32 %2, %6, %6 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]\n\t"
+            "v_pk_add_f32 %3, %7, %7 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+            : "=&v"(u6), "=&v"(u9), "=&v"(u11), "=v"(u14)
+            : "v"(v[6]), "v"(v[9]), "v"(v[11]), "v"(v[14]));
+    v[5] = __builtin_elementwise_fma(v[5].yx, (pf2){s1, -s1}, t5);
+    v[7] = __builtin_elementwise_fma(v[7].yx, (pf2){s3, -s3}, t7);
+    v[13] = __builtin_elementwise_fma(v[13].yx, (pf2){s3, -s3}, t13);
+    v[15] = __builtin_elementwise_fma(v[15].yx, (pf2){-s1, s1}, t15);
+    v[6] = u6 * R2;
+    v[9] = u9 * R2;
+    v[11] = u11 * (-R2);
+    v[14] = u14 * (-R2);
+#endif
 }
 // second radix-4 stage over positions 4 m1 + k1 (k1 = 0..3), m1 = 2 with the
 // W16^4 twiddle of position 10 folded in
