@@ -30,6 +30,28 @@ __device__ __forceinline__ float2 upd_coef_safe(float a, float c, float m, float
 }
 __device__ __forceinline__ float2 slot_update(float2 f, float2 o, float2 p, float pm, const DevState &st,
                                               float2 &num, float &oa) {
+#if !defined(FPM_UPD_CHAIN) && !defined(FPM_UPD_SQUARED)
+    // The same operations as the chain below, the object and the pupil
+    // coefficient computed side by side: every transcendental is followed by
+    // the other chain's independent one instead of its own use (a trans-use
+    // hazard wait state each time in the chained order), and never more than
+    // two in a row (four in a row measured slower).
+    const pf2 po = pin(o), pp = pin(p);
+    const float pa2 = cabs2(p), oa2 = cabs2(o);
+    const float pa = __builtin_amdgcn_sqrtf(pa2);
+    oa = __builtin_amdgcn_sqrtf(oa2);
+    const pf2 D = pin(f) - pmul(po, pp);
+    const float ap = __builtin_fmaf(pa, pa, st.delta2), ao = __builtin_fmaf(oa, oa, st.delta1);
+    const float rp = __builtin_amdgcn_rcpf(ap), ro = __builtin_amdgcn_rcpf(ao);
+    const pf2 dp = pmulc(D, pp), dq = pmulc(D, po);
+    const float qp = st.d2_im * rp, qo = st.d1_im * ro;
+    const float xp = __builtin_fmaf(qp, qp, 1.0f) * pm, xo = __builtin_fmaf(qo, qo, 1.0f) * 1.0f;
+    const float sp0 = __builtin_amdgcn_rcpf(xp), so0 = __builtin_amdgcn_rcpf(xo);
+    const float fp = rp * pa, fo = ro * oa;
+    const float sp = sp0 * fp, so = so0 * fo;
+    num = pout(pmul(dq, (pf2){so, -qo * so}));
+    return pout(po + pmul(dp, (pf2){sp, -qp * sp}));
+#else
     const pf2 po = pin(o), pp = pin(p);
     const pf2 D = pin(f) - pmul(po, pp);
     const float pa = cmag(p);
@@ -39,6 +61,7 @@ __device__ __forceinline__ float2 slot_update(float2 f, float2 o, float2 p, floa
     const float2 co = upd_coef_safe(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f, oa);
     num = pout(pmul(pmulc(D, po), pin(co)));
     return pout(nv);
+#endif
 }
 
 }  // namespace fpm
