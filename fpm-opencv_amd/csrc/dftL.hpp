@@ -6,6 +6,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
+#include "cpk.hpp"
 #include "dft16.hpp"
 #include "fft_lds.hpp"
 
@@ -32,6 +35,15 @@ __device__ __forceinline__ LdsTw fresh_tw(const LdsTw &w) { return LdsTw{fresh_l
 template <bool INV, bool HX = false, typename TW>
 __device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], float2 *scr,
                                             const TW &wt, int t, int xrd) {
+#ifndef FPM_DFTL_SCALAR
+    constexpr bool packed = !std::is_same_v<TW, LdsTw>;
+#else
+    constexpr bool packed = false;
+#endif
+    if constexpr (!packed) {
+    // scalar float2 butterflies, one cmul per twiddle: the Np 1024 kernels
+    // (LDS twiddles; memory-bound) measured 4 % slower with the packed form
+    // (config 5: 58.5-58.9 vs 56.1-56.6 ms of LED steps per iteration)
     float2 y[16];
     dft16<INV>(v, y);
     const auto &w = fresh_tw(wt);
@@ -43,6 +55,34 @@ __device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], 
     else
         exchange16(scr, t, xrd, y, z);
     dft16<INV>(z, out);
+    } else {
+    // packed FP32 (cpk.hpp), the twiddles in asm blocks of five (products,
+    // then fmas): objCrop (register twiddles) 0.658 -> 0.636 ms per step
+    pf2 pv[16], py[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pv[k] = pin(v[k]);
+    pdft16<INV>(pv, py);
+    const auto &w = fresh_tw(wt);
+#pragma unroll
+    for (int m0 = 1; m0 < 16; m0 += 5) {
+        pf2 w5[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) w5[i] = pin(w[m0 + i]);
+        ptw_block<INV, 5>(&py[m0], w5);
+    }
+    float2 y[16], z[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) y[k] = pout(py[k]);
+    if constexpr (HX)
+        exchange16_half(scr, t, xrd, y, z);
+    else
+        exchange16(scr, t, xrd, y, z);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pv[k] = pin(z[k]);
+    pdft16<INV>(pv, py);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) out[k] = pout(py[k]);
+    }
 }
 
 template <int M, bool INV>
