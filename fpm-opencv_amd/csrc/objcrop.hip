@@ -107,14 +107,44 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
     float2 *base = io + (size_t)b * L * L + c0;
     constexpr int NTH = 16 * G;
     float2 x[M][16];
+    constexpr int G2 = G / 2;
+#ifdef FPM_CROP_PRELOAD
+    // both halves' strip loads issued before the first barrier (twice the
+    // bytes in flight per block), parked in registers until their half's
+    // LDS round
+    constexpr int NLD = (H * G2 + NTH - 1) / NTH;
+    float4 qh[2][NLD];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int idx = ya * G2 + threadIdx.x + k * NTH;
+            if (idx < (yb + 1) * G2) {
+                const int y = idx / G2, cc = 2 * (idx - y * G2);
+                qh[h][k] = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
+            }
+        }
+    }
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         // objF row y + h H is spec row y + (1 - h) H: the live rows of this
         // half are the contiguous range [ya, yb]
         const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
+#ifdef FPM_CROP_PRELOAD
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int idx = ya * G2 + threadIdx.x + k * NTH;
+            if (idx < (yb + 1) * G2) {
+                const int y = idx / G2, cc = 2 * (idx - y * G2);
+                strip[y * SP + cc] = make_float2(qh[h][k].x, qh[h][k].y);
+                strip[y * SP + cc + 1] = make_float2(qh[h][k].z, qh[h][k].w);
+            }
+        }
+#else
         // strip load: consecutive threads take consecutive column pairs of a row
         // (16-byte loads: twice the bytes in flight per load instruction)
-        constexpr int G2 = G / 2;
 FPM_CROP_PRAGMA_UNROLL
         for (int idx = ya * G2 + threadIdx.x; idx < (yb + 1) * G2; idx += NTH) {
             const int y = idx / G2, cc = 2 * (idx - y * G2);
@@ -122,6 +152,7 @@ FPM_CROP_PRAGMA_UNROLL
             strip[y * SP + cc] = make_float2(q.x, q.y);
             strip[y * SP + cc + 1] = make_float2(q.z, q.w);
         }
+#endif
         __syncthreads();
 #pragma unroll
         for (int j = 8 * h; j < 8 * h + 8; ++j)
