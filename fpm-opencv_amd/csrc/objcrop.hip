@@ -108,51 +108,59 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
     constexpr int NTH = 16 * G;
     float2 x[M][16];
     constexpr int G2 = G / 2;
-#ifdef FPM_CROP_PRELOAD
-    // both halves' strip loads issued before the first barrier (twice the
-    // bytes in flight per block), parked in registers until their half's
-    // LDS round
-    constexpr int NLD = (H * G2 + NTH - 1) / NTH;
+    // Both halves' strip loads are issued before the first barrier (twice
+    // the bytes in flight per block), parked in registers until their half's
+    // LDS round: objCrop 0.636 -> 0.584 ms per step at the metric config
+    // (same box, profiles/r03_ab/crop_preload_ab.txt).  L = 1024 would need
+    // 257 VGPRs for it and keeps the per-half loads (FPM_CROP_NO_PRELOAD
+    // selects them everywhere for A/B runs).
+#ifndef FPM_CROP_NO_PRELOAD
+    constexpr bool PRELOAD = M <= 3;
+#else
+    constexpr bool PRELOAD = false;
+#endif
+    constexpr int NLD = PRELOAD ? (H * G2 + NTH - 1) / NTH : 1;
     float4 qh[2][NLD];
+    if constexpr (PRELOAD) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
+        for (int h = 0; h < 2; ++h) {
+            const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
 #pragma unroll
-        for (int k = 0; k < NLD; ++k) {
-            const int idx = ya * G2 + threadIdx.x + k * NTH;
-            if (idx < (yb + 1) * G2) {
-                const int y = idx / G2, cc = 2 * (idx - y * G2);
-                qh[h][k] = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
+            for (int k = 0; k < NLD; ++k) {
+                const int idx = ya * G2 + threadIdx.x + k * NTH;
+                if (idx < (yb + 1) * G2) {
+                    const int y = idx / G2, cc = 2 * (idx - y * G2);
+                    qh[h][k] = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
+                }
             }
         }
     }
-#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         // objF row y + h H is spec row y + (1 - h) H: the live rows of this
         // half are the contiguous range [ya, yb]
         const int ya = max(sy0 - (1 - h) * H, 0), yb = min(sy1 - (1 - h) * H, H - 1);
-#ifdef FPM_CROP_PRELOAD
+        if constexpr (PRELOAD) {
 #pragma unroll
-        for (int k = 0; k < NLD; ++k) {
-            const int idx = ya * G2 + threadIdx.x + k * NTH;
-            if (idx < (yb + 1) * G2) {
+            for (int k = 0; k < NLD; ++k) {
+                const int idx = ya * G2 + threadIdx.x + k * NTH;
+                if (idx < (yb + 1) * G2) {
+                    const int y = idx / G2, cc = 2 * (idx - y * G2);
+                    strip[y * SP + cc] = make_float2(qh[h][k].x, qh[h][k].y);
+                    strip[y * SP + cc + 1] = make_float2(qh[h][k].z, qh[h][k].w);
+                }
+            }
+        } else {
+            // strip load: consecutive threads take consecutive column pairs of a row
+            // (16-byte loads: twice the bytes in flight per load instruction)
+FPM_CROP_PRAGMA_UNROLL
+            for (int idx = ya * G2 + threadIdx.x; idx < (yb + 1) * G2; idx += NTH) {
                 const int y = idx / G2, cc = 2 * (idx - y * G2);
-                strip[y * SP + cc] = make_float2(qh[h][k].x, qh[h][k].y);
-                strip[y * SP + cc + 1] = make_float2(qh[h][k].z, qh[h][k].w);
+                const float4 q = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
+                strip[y * SP + cc] = make_float2(q.x, q.y);
+                strip[y * SP + cc + 1] = make_float2(q.z, q.w);
             }
         }
-#else
-        // strip load: consecutive threads take consecutive column pairs of a row
-        // (16-byte loads: twice the bytes in flight per load instruction)
-FPM_CROP_PRAGMA_UNROLL
-        for (int idx = ya * G2 + threadIdx.x; idx < (yb + 1) * G2; idx += NTH) {
-            const int y = idx / G2, cc = 2 * (idx - y * G2);
-            const float4 q = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
-            strip[y * SP + cc] = make_float2(q.x, q.y);
-            strip[y * SP + cc + 1] = make_float2(q.z, q.w);
-        }
-#endif
         __syncthreads();
 #pragma unroll
         for (int j = 8 * h; j < 8 * h + 8; ++j)
