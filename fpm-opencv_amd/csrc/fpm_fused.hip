@@ -512,6 +512,22 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
                 }
                 const unsigned iw[8] = {cI[0].x, cI[0].y, cI[0].z, cI[0].w, cI[1].x, cI[1].y, cI[1].z, cI[1].w};
+#ifdef FPM_AMP_PIPE  // A/B: software-pipelined (pixel m's v_rsq, then pixel m + 1's eps add and magnitude)
+                {
+                    auto Ipx = [&](int m2) { return (float)((m2 & 1) ? (iw[m2 >> 1] >> 16) : (iw[m2 >> 1] & 0xffffu)); };
+                    auto qof = [&](int m2) {
+                        const pf2 tt = pin(r[m2]) + (pf2){epsn, epsn_im};
+                        return __builtin_fmaf(__builtin_fmaf(tt.x, tt.x, tt.y * tt.y), Ipx(m2), 1.17549435e-38f);
+                    };
+                    float q = qof(0);
+#pragma unroll
+                    for (int m2 = 0; m2 < 16; ++m2) {
+                        const float rs = __builtin_amdgcn_rsqf(q);
+                        if (m2 + 1 < 16) q = qof(m2 + 1);
+                        v[m2] = pout(pin(r[m2]) * (Ipx(m2) * rs));
+                    }
+                }
+#else
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
                     const float Iv = (float)((m2 & 1) ? (iw[m2 >> 1] >> 16) : (iw[m2 >> 1] & 0xffffu));
@@ -523,6 +539,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     const float sc = amp_scale(mag2, Iv);
                     v[m2] = pout(pin(r[m2]) * sc);
                 }
+#endif
                 float2 o[6];
                 dft256_out6<HALF>(v, o, scr, wt, t, xrd);
 #pragma unroll
