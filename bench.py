@@ -310,8 +310,8 @@ def cpu_baseline(geo, stack_host, threads, cores_note):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)  # ~0.2 s of GPU time at the metric config
+    ap.add_argument("--warmup", type=int, default=5)  # the first launches after setup run slower (clock ramp)
     ap.add_argument("--patches", type=int, default=0, help="patches per GPU (0: 256, 8 for --config c5, 64 for c2)")
     ap.add_argument("--patches-total", type=int, default=0,
                     help="strong scaling: one field of T patches sharded over the ranks (parallel.shard_range), "
