@@ -5,12 +5,15 @@ Workload (SURVEY.md 8(d) metric config): dataset_dogStomach optics
 (6.5 um pixel, mag 8.1485, objNA 0.1, lambda 0.6292), all 293 LEDs of its
 holeCoordinates array (maxIlluminationNA raised to 0.6), cropSizeX Np = 256
 -> resImprovementFactor 3, L = 768, naRadius 33, delta1 = 10, delta2 = 3,
-256 independent patches per GPU (weak scaling: every rank owns its own 256
-patches), synthetic seeded forward-model stacks resident in HBM.
+and north_star's fixed field of 256 independent patches: at N GPUs it is
+statically sharded over the ranks (fpm_amd.parallel.shard_range: 256 / 128 /
+64 / 32 patches per rank at N = 1 / 2 / 4 / 8; strong scaling), synthetic
+seeded forward-model stacks resident in HBM.  `--weak` gives every rank its
+own --patches (BASELINE config 4: `--patches-total 1024`, 128 per rank at 8).
 
 One step = one runFPM iteration (fpmMain.cpp:345-482) over every patch:
 293 sequential LED updates per patch plus the per-iteration objCrop IDFT.
-value = patches x LEDs x steps x n_gpus / (max over ranks of the timed wall
+value = field patches x LEDs x steps / (max over ranks of the timed wall
 time).  Launch: `python bench.py` (1 GPU) or torch.distributed.run with
 --nproc-per-node N (one rank per GPU, RCCL).  After the timed region, ranks
 > 0 send their objCrop tiles to rank 0 with one RCCL gather (the stitched-field
@@ -312,10 +315,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)  # ~0.2 s of GPU time at the metric config
     ap.add_argument("--warmup", type=int, default=5)  # the first launches after setup run slower (clock ramp)
-    ap.add_argument("--patches", type=int, default=0, help="patches per GPU (0: 256, 8 for --config c5, 64 for c2)")
+    ap.add_argument("--patches", type=int, default=0,
+                    help="--weak: patches per GPU (0: 256, 8 for --config c5, 64 for c2)")
     ap.add_argument("--patches-total", type=int, default=0,
                     help="strong scaling: one field of T patches sharded over the ranks (parallel.shard_range), "
-                         "gathered and stitched on rank 0 after the timed region; 0 = weak scaling (--patches per rank)")
+                         "gathered and stitched on rank 0 after the timed region (0: north_star's 256-patch field "
+                         "for --config metric, weak scaling for the other configs)")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: every rank owns --patches patches")
     ap.add_argument("--np", type=int, default=256)
     ap.add_argument("--config", default="metric", choices=["metric", "c2", "c3", "c5"],
                     help="workload (config_geometry); only 'metric' is the headline line")
@@ -375,7 +381,9 @@ def main():
 
     geo = config_geometry(args.config, args.np)
     fp16 = args.fp16 or args.config == "c5"
-    strong = args.patches_total > 0
+    if args.patches_total <= 0 and not args.weak and args.config == "metric":
+        args.patches_total = 256  # north_star: a 256-patch x 293-LED stack at 1/2/4/8 GPUs
+    strong = args.patches_total > 0 and not args.weak
     if strong:
         # strong scaling: one fixed field of T patches, contiguous shards
         # (parallel.shard_range); data seeded per global patch
@@ -447,7 +455,7 @@ def main():
     roofline = roofline_line(geo, info, per_launch_ms, per_launch_updates, args.pmc or default_pmc(args, info))
 
     gather = None
-    if (world > 1 or strong) and not args.no_gather:
+    if world > 1 and not args.no_gather:
         # the final exchange of SURVEY.md 8(e): every rank's objCrop tiles to
         # rank 0 in one gather (RCCL over xGMI), then -- for a fixed field --
         # the stitched high-resolution field on rank 0's GPU; timed beside

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "../../include/fpm_hip.h"
+#include "../../include/fpm_hip_debug.h"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
 
@@ -50,10 +52,9 @@ hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas
                                         const FftPlan &pl, unsigned long long *dbg, hipStream_t s);
 // Np 1024 register row/column kernels of the general path (np1024.hip)
 bool np1024_supported(int np, int r);
-size_t fused_park_elems(int nt, int B);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  float2 *pscr, int nt, int ks, unsigned long long *dbg, float2 *xch, int *flags,
+                                  int ks, unsigned long long *dbg, float2 *xch, int *flags, int stall_led,
                                   hipStream_t s);
 size_t fused_xch_elems(int B, int ks);
 size_t fused_flag_words(int B, int ks);
@@ -63,7 +64,7 @@ size_t fused_dist_elems(int B, int ks);
 int fused_dist_parts(int B, int n_cu, int r, int L);
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, hipStream_t s);
+                             float2 *area, int *flags, int stall_led, hipStream_t s);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 bool meas_layout_copy(const uint16_t *src, uint16_t *dst, int np, int g, size_t nimg, hipStream_t s,
@@ -139,12 +140,12 @@ struct fpm_ctx {
     int meas_g = 0;                 // meas holds the column layout of meas_layout with g-lane groups
                                     // once uploaded (16: Np 256, 10: Np 200, Np: the small-patch
                                     // kernel and the Np 1024 general path, transposed); 0: C-ABI
-    float2 *pscr = nullptr;         // fused path: lane-private parking of P / F
-    int fused_nt = 0;               // fused kernel threads per workgroup (512 / 1024)
+    int fused_nt = 0;               // Np 256 fused kernel: threads per workgroup (512), 0 = not used
     int split_ks = 1;               // split / distributed mode: workgroups per patch (2, 4, 8), else 1
     bool dist = false;              // distributed mode (fused_dist.hip) instead of split mode
     float2 *xch = nullptr;          //   exchange area
     int *split_flags = nullptr;     //   handoff flags [KS B] + sticky abort flag + XCC ids [KS B]
+    int stall_led = -1;             //   fpm_debug_set_stall (tests): the last part stops publishing
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
@@ -353,8 +354,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     // Np 90 (configs 1 / 2): the register-transform kernel unless FPM_NO_S90=1
     // selects the generic small-patch kernel
     c->fused_s90 = !c->fused_nt && !c->fused_mr && !getenv("FPM_NO_S90") && fused_s90_supported(np, r, st);
-    c->fused_small = !c->fused_nt && !c->fused_mr && !c->fused_s90 && !getenv("FPM_NO_SMALL") &&
-                     fused_small_supported(np, r, st);
+    c->fused_small = !c->fused_nt && !c->fused_mr && !c->fused_s90 && fused_small_supported(np, r, st);
     const bool fused_ok = c->fused_nt || c->fused_mr || c->fused_s90 || c->fused_small;
     if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_ok))
         return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
@@ -410,16 +410,14 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     } else {
         c->meas_g = c->fused_small ? np : c->fused_s90 ? 9 : c->fused_mr ? 10 : 16;
         if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
-        if ((rc = dalloc(c, &c->pscr, fused_park_elems(c->fused_nt, B)))) return fail(rc);
-        int n_cu = 0, coop = 0;
+        int n_cu = 0;
         (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
-        (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device);
         // small batches: every phase distributed over KS workgroups per patch
         // (fused_dist.hip), else split mode (column parts only), else one
         // workgroup per patch
-        const int dks = (c->fused_nt == 512 && coop) ? fused_dist_parts(B, n_cu, r, L) : 0;
+        const int dks = c->fused_nt ? fused_dist_parts(B, n_cu, r, L) : 0;
         c->dist = dks > 1;
-        c->split_ks = c->dist ? dks : (c->fused_nt && coop) ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
+        c->split_ks = c->dist ? dks : c->fused_nt ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
         if (c->split_ks > 1) {
             const size_t nx = c->dist ? fused_dist_elems(B, c->split_ks) : fused_xch_elems(B, c->split_ks);
             if ((rc = dalloc(c, &c->xch, nx))) return fail(rc);
@@ -704,11 +702,11 @@ int fpm_run(fpm_ctx *c, int iters) {
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED && c->dist) {
             HIP_TRY(launch_fused_dist(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev, c->prob.n_order, c->tw_np,
-                                      c->split_ks, c->dbg, c->xch, c->split_flags, c->stream));
+                                      c->split_ks, c->dbg, c->xch, c->split_flags, c->stall_led, c->stream));
         } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
-                                           c->prob.n_order, c->tw_np, c->pscr, c->fused_nt, c->split_ks,
-                                           c->dbg, c->xch, c->split_flags, c->stream));
+                                           c->prob.n_order, c->tw_np, c->split_ks, c->dbg, c->xch,
+                                           c->split_flags, c->stall_led, c->stream));
         } else if (use_graph) {
             HIP_TRY(launch_general_graphs(c, c->stream));
         } else {
@@ -851,6 +849,19 @@ int fpm_download_objcrop_device(fpm_ctx *c, float *dst) {
     return FPM_OK;
 }
 
+int fpm_abi_version(void) { return FPM_ABI_VERSION; }
+
+int fpm_get_info_sized(const fpm_ctx *c, fpm_info *info, size_t info_size) {
+    if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
+    if (info_size < offsetof(fpm_info, fused_kernel))
+        return set_err(FPM_ERR_INVAL, "fpm_info of %zu bytes predates every released layout", info_size);
+    fpm_info full;
+    const int rc = fpm_get_info(c, &full);
+    if (rc) return rc;
+    std::memcpy(info, &full, std::min(info_size, sizeof full));
+    return FPM_OK;
+}
+
 int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
     if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
     info->path = c->path;
@@ -865,12 +876,22 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
                          : c->fused_mr         ? FPM_KERNEL_FUSED_NP200
                          : c->dist             ? FPM_KERNEL_FUSED_NP256_DIST
                                                : FPM_KERNEL_FUSED_NP256;
+    info->threads_per_wg = c->path != FPM_PATH_FUSED ? 0
+                           : c->fused_s90 || c->fused_small ? 1024
+                           : c->fused_mr ? 768
+                                         : c->fused_nt;
     return FPM_OK;
 }
 
 int fpm_get_timing(const fpm_ctx *c, fpm_timing *t) {
     if (!c || !t) return set_err(FPM_ERR_INVAL, "null argument");
     *t = c->timing;
+    return FPM_OK;
+}
+
+int fpm_debug_set_stall(fpm_ctx *c, int led) {
+    if (!c) return set_err(FPM_ERR_INVAL, "null ctx");
+    c->stall_led = led;
     return FPM_OK;
 }
 

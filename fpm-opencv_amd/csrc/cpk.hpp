@@ -35,13 +35,9 @@ __device__ __forceinline__ float2 pout(pf2 a) { return __builtin_bit_cast(float2
 // table) where rsq(mag2 * rcp(I)) needed two; the fma costs what the mul did.
 // FLT_MIN keeps I = 0 finite: 0 * rsq(FLT_MIN) = 0, the reference's sqrt(0)
 // factor (it is below the rounding of mag2 I for any I >= 1 and mag2 the
-// solver meets).  -DFPM_AMP_RCP builds the two-transcendental form for A/B runs.
+// solver meets).
 __device__ __forceinline__ float amp_scale(float mag2, float I) {
-#ifdef FPM_AMP_RCP
-    return __builtin_amdgcn_rsqf(mag2 * __builtin_amdgcn_rcpf(I));
-#else
     return I * __builtin_amdgcn_rsqf(__builtin_fmaf(mag2, I, 1.17549435e-38f));
-#endif
 }
 
 // a + W4 b with W4 = -i (forward) or +i (inverse):
@@ -152,42 +148,13 @@ __device__ __forceinline__ void ptw_range(pf2 (&a)[M > 0 ? M : 1], const pf2 (&w
         i += len;
     }
 }
-// A/B (FPM_TW_ONE): all fifteen in ONE asm block (three groups of five
-// products, then their fmas): no compiler padding at block boundaries
-template <bool CONJ>
-__device__ __forceinline__ void ptw15_one(pf2 (&a)[16], const pf2 (&w)[16]) {
-    pf2 t0, t1, t2, t3, t4;
-    if constexpr (CONJ)
-        asm(FPM_TWMUL_C(0, 5, 20) FPM_TWMUL_C(1, 6, 21) FPM_TWMUL_C(2, 7, 22) FPM_TWMUL_C(3, 8, 23) FPM_TWMUL_C(4, 9, 24) FPM_TWFMA_C(5, 20, 0) FPM_TWFMA_C(6, 21, 1) FPM_TWFMA_C(7, 22, 2) FPM_TWFMA_C(8, 23, 3) FPM_TWFMA_C(9, 24, 4) FPM_TWMUL_C(0, 10, 25) FPM_TWMUL_C(1, 11, 26) FPM_TWMUL_C(2, 12, 27) FPM_TWMUL_C(3, 13, 28) FPM_TWMUL_C(4, 14, 29) FPM_TWFMA_C(10, 25, 0) FPM_TWFMA_C(11, 26, 1) FPM_TWFMA_C(12, 27, 2) FPM_TWFMA_C(13, 28, 3) FPM_TWFMA_C(14, 29, 4) FPM_TWMUL_C(0, 15, 30) FPM_TWMUL_C(1, 16, 31) FPM_TWMUL_C(2, 17, 32) FPM_TWMUL_C(3, 18, 33) FPM_TWMUL_C(4, 19, 34) FPM_TWFMA_C(15, 30, 0) FPM_TWFMA_C(16, 31, 1) FPM_TWFMA_C(17, 32, 2) FPM_TWFMA_C(18, 33, 3) FPM_TWFMA_C(19, 34, 4)
-            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]),
-              "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]),
-              "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
-            : "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]), "v"(w[9]),
-              "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]));
-    else
-        asm(FPM_TWMUL_F(0, 5, 20) FPM_TWMUL_F(1, 6, 21) FPM_TWMUL_F(2, 7, 22) FPM_TWMUL_F(3, 8, 23) FPM_TWMUL_F(4, 9, 24) FPM_TWFMA_F(5, 20, 0) FPM_TWFMA_F(6, 21, 1) FPM_TWFMA_F(7, 22, 2) FPM_TWFMA_F(8, 23, 3) FPM_TWFMA_F(9, 24, 4) FPM_TWMUL_F(0, 10, 25) FPM_TWMUL_F(1, 11, 26) FPM_TWMUL_F(2, 12, 27) FPM_TWMUL_F(3, 13, 28) FPM_TWMUL_F(4, 14, 29) FPM_TWFMA_F(10, 25, 0) FPM_TWFMA_F(11, 26, 1) FPM_TWFMA_F(12, 27, 2) FPM_TWFMA_F(13, 28, 3) FPM_TWFMA_F(14, 29, 4) FPM_TWMUL_F(0, 15, 30) FPM_TWMUL_F(1, 16, 31) FPM_TWMUL_F(2, 17, 32) FPM_TWMUL_F(3, 18, 33) FPM_TWMUL_F(4, 19, 34) FPM_TWFMA_F(15, 30, 0) FPM_TWFMA_F(16, 31, 1) FPM_TWFMA_F(17, 32, 2) FPM_TWFMA_F(18, 33, 3) FPM_TWFMA_F(19, 34, 4)
-            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]),
-              "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]),
-              "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
-            : "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]), "v"(w[9]),
-              "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]));
-}
 template <bool CONJ, class TW>
 __device__ __forceinline__ void ptwiddle15(pf2 (&py)[16], const TW &wt) {
-#ifndef FPM_TW_SINGLE  // A/B: one asm fma per twiddle (round 2)
     pf2 w[16];
 #pragma unroll
     for (int m = 1; m < 16; ++m) w[m] = pin(wt[m]);
     w[0] = w[1];
-#ifdef FPM_TW_ONE
-    ptw15_one<CONJ>(py, w);
-#else
     ptw_range<CONJ, 16>(py, w);
-#endif
-#else
-#pragma unroll
-    for (int m = 1; m < 16; ++m) py[m] = CONJ ? pmulc(py[m], pin(wt[m])) : pmul(py[m], pin(wt[m]));
-#endif
 }
 
 // radix-4 butterfly in place (the scalar dft4 of fft_lds.hpp, packed)
@@ -233,16 +200,6 @@ __device__ __forceinline__ pf2 pw16(pf2 a) {
 // position k1 + 4 m1 *= W16^{k1 m1}; position 10 (W16^4) is left to pbf4_w2
 template <bool INV>
 __device__ __forceinline__ void pmid_tw(pf2 (&v)[16]) {
-#ifdef FPM_MID_SERIAL  // A/B: one twiddle after the other (round 2)
-    v[5] = pw16<INV, 1>(v[5]);
-    v[6] = pw16<INV, 2>(v[6]);
-    v[7] = pw16<INV, 3>(v[7]);
-    v[9] = pw16<INV, 2>(v[9]);
-    v[11] = pw16<INV, 6>(v[11]);
-    v[13] = pw16<INV, 3>(v[13]);
-    v[14] = pw16<INV, 6>(v[14]);
-    v[15] = pw16<INV, 9>(v[15]);
-#else
     // the same operations, first steps of all eight twiddles before the
     // second steps (no VOP3P read right after the write it depends on; the
     // four W4 rotations in one asm block: no padding between blocks)
@@ -272,7 +229,6 @@ __device__ __forceinline__ void pmid_tw(pf2 (&v)[16]) {
     v[9] = u9 * R2;
     v[11] = u11 * (-R2);
     v[14] = u14 * (-R2);
-#endif
 }
 // second radix-4 stage over positions 4 m1 + k1 (k1 = 0..3), m1 = 2 with the
 // W16^4 twiddle of position 10 folded in

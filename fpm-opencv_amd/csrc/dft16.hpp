@@ -90,10 +90,7 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], float2 (&r)[16]) {
 // row t starts at dword 36 t = 4 (9 t mod 16) (mod 64), a distinct 16-byte
 // slot for each t, and every ds_read_b128 lane group holds 16 distinct t, so
 // the wide reads are conflict-free; the 16-lane row writes stay contiguous.
-#ifndef FPM_XP
-#define FPM_XP 18
-#endif
-constexpr int XP = FPM_XP;                  // exchange-tile row pitch
+constexpr int XP = 18;                      // exchange-tile row pitch
 constexpr int XTILE = 16 * XP;              // complex per group tile
 __device__ __forceinline__ int opaque_int(int v) {
     asm volatile("" : "+v"(v));
@@ -104,31 +101,14 @@ __device__ __forceinline__ int exch_rbase(int t) { return opaque_int(t * XP); }
 // (a lane-major tile with eight 16-byte writes per lane was measured: pass B
 // +3%, the strided reads cost more than the halved write count saves)
 __device__ __forceinline__ void exchange16(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
-    (void)t;
-#if defined(FPM_EXP_NOXCHG)  // timing experiment only (wrong results): no LDS exchange
-#pragma unroll
-    for (int j = 0; j < 16; ++j) z[j] = y[j ^ 5];
-    return;
-#elif defined(FPM_EXP_WRONLY)  // timing experiment only: writes, no reads
 #pragma unroll
     for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
+    const float4 *rp = (const float4 *)(scr + xrd);  // 16-B aligned: XTILE and XP even
 #pragma unroll
-    for (int j = 0; j < 16; ++j) z[j] = y[j ^ 5];
-    return;
-#endif
-#pragma unroll
-    for (int m1 = 0; m1 < 16; ++m1) scr[m1 * XP + t] = y[m1];
-    if constexpr (XP % 2 == 0) {
-        const float4 *rp = (const float4 *)(scr + xrd);  // 16-B aligned: XTILE and XP even
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float4 q = rp[j];
-            z[2 * j] = make_float2(q.x, q.y);
-            z[2 * j + 1] = make_float2(q.z, q.w);
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) z[j] = scr[xrd + j];
+    for (int j = 0; j < 8; ++j) {
+        const float4 q = rp[j];
+        z[2 * j] = make_float2(q.x, q.y);
+        z[2 * j + 1] = make_float2(q.z, q.w);
     }
 }
 

@@ -218,7 +218,6 @@ __device__ __forceinline__ void dft200(float2 (&v)[20], float2 *tile, const floa
     for (int k = 0; k < 20; ++k) p[k] = pin(v[k]);
     if (IN6) dft20_in6<INV>(p);
     else dft20<INV>(p);
-#ifndef FPM_TW200_SINGLE  // A/B: one pmul / pmulc per twiddle
     {
         pf2 w[20];
 #pragma unroll
@@ -226,13 +225,6 @@ __device__ __forceinline__ void dft200(float2 (&v)[20], float2 *tile, const floa
         w[0] = w[1];
         ptw_range<INV, 20>(p, w);  // cpk.hpp: blocks of products, then fmas
     }
-#else
-#pragma unroll
-    for (int m1 = 1; m1 < 20; ++m1) {
-        const pf2 w = pin(tw2[m1 * 10 + l]);
-        p[m1] = INV ? pmulc(p[m1], w) : pmul(p[m1], w);
-    }
-#endif
     float2 u[20];
 #pragma unroll
     for (int k = 0; k < 20; ++k) u[k] = pout(p[k]);

@@ -68,19 +68,11 @@ __device__ __forceinline__ void dft90_ab(float2 (&v)[10], float2 *tile, const fl
 #pragma unroll
     for (int k = 0; k < 9; ++k) p[k] = pin(v[k]);
     dft9<INV>(p);
-#ifndef FPM_TW90_SINGLE  // twiddles in asm pairs (cpk.hpp ptw_block), each pair read just before it
 #pragma unroll
     for (int m1 = 1; m1 < 9; m1 += 2) {
         const pf2 w[2] = {pin(tw[m1 * 10 + l]), pin(tw[(m1 + 1) * 10 + l])};
         ptw_block<INV, 2>(&p[m1], w);
     }
-#else
-#pragma unroll
-    for (int m1 = 1; m1 < 9; ++m1) {
-        const pf2 w = pin(tw[m1 * 10 + l]);
-        p[m1] = INV ? pmulc(p[m1], w) : pmul(p[m1], w);
-    }
-#endif
 #pragma unroll
     for (int m1 = 0; m1 < 9; ++m1) tile[m1 * kXP90 + l] = pout(p[m1]);
     // lane j reads row j (lane 9: row 9, never written -- its output is unused)
@@ -105,20 +97,12 @@ __device__ __forceinline__ void dft90_ba(float2 (&v)[10], float2 *tile, const fl
 #pragma unroll
     for (int k = 0; k < 10; ++k) p[k] = pin(v[k]);
     dft10<INV>(p);
-#ifndef FPM_TW90_SINGLE
 #pragma unroll
     for (int m = 1; m < 9; m += 2) {
         const pf2 w[2] = {pin(tw[m * 10 + l]), pin(tw[(m + 1) * 10 + l])};
         ptw_block<INV, 2>(&p[m], w);
     }
     p[9] = INV ? pmulc(p[9], pin(tw[90 + l])) : pmul(p[9], pin(tw[90 + l]));
-#else
-#pragma unroll
-    for (int m = 1; m < 10; ++m) {
-        const pf2 w = pin(tw[m * 10 + l]);
-        p[m] = INV ? pmulc(p[m], w) : pmul(p[m], w);
-    }
-#endif
     // row m, column j; lane 9 writes the pad column (never read)
 #pragma unroll
     for (int m = 0; m < 10; ++m) tile[m * kXP90 + l] = pout(p[m]);

@@ -35,11 +35,7 @@ __device__ __forceinline__ LdsTw fresh_tw(const LdsTw &w) { return LdsTw{fresh_l
 template <bool INV, bool HX = false, typename TW>
 __device__ __forceinline__ void dft256_full(float2 (&v)[16], float2 (&out)[16], float2 *scr,
                                             const TW &wt, int t, int xrd) {
-#ifndef FPM_DFTL_SCALAR
     constexpr bool packed = !std::is_same_v<TW, LdsTw>;
-#else
-    constexpr bool packed = false;
-#endif
     if constexpr (!packed) {
     // scalar float2 butterflies, one cmul per twiddle: the Np 1024 kernels
     // (LDS twiddles; memory-bound) measured 4 % slower with the packed form

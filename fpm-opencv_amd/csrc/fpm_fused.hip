@@ -55,29 +55,25 @@ namespace fpm {
 constexpr int n_parts(int ks) { return ks == 1 ? 2 : ks; }
 constexpr int part_cols(int ks) { return fz::NP / n_parts(ks); }
 
-// Kernel configurations:
-//   NT = 512  : 32 groups, 2 FFT rows each, 2 waves per SIMD (256 VGPRs), full
-//               exchange tiles, measurement and T slots prefetched one pass-B
-//               column ahead, P and F in registers throughout.
-//   NT = 1024 : 64 groups, 1 FFT row each, 4 waves per SIMD (128 VGPRs), half
-//               exchange tiles (xchg), no prefetch (the other waves of the
-//               SIMD hide the latency), and P / F parked in a lane-private
-//               global scratch while pass B runs so they hold no registers.
+// Kernel configuration (NT = 512): 32 groups, 2 FFT rows each, 2 waves per
+// SIMD (256 VGPRs), full exchange tiles, T slots prefetched one pass-B column
+// ahead, P and F in registers throughout.  (A 1024-thread variant at 4 waves
+// per SIMD -- half exchange tiles, P / F parked in global scratch -- measured
+// 28 % slower and was removed in round 4)
 template <int NT>
 struct FzCfg {
+    static_assert(NT == 512, "512 threads per workgroup");
     static constexpr int NG = NT / 16;            // 16-lane groups
     static constexpr int RPG = fz::NROWS / NG;    // FFT rows per group
     static constexpr int NW = NT / 64;            // waves
-    static constexpr bool HALF = NT > 512;        // half exchange tiles
-    static constexpr bool PARK = NT > 512;        // P / F parked across pass B
-    static constexpr int XT = HALF ? 8 * XP : XTILE;  // exchange tile per group (complex)
+    static constexpr int XT = XTILE;              // exchange tile per group (complex)
 };
 
 // store the column part h of a row IDFT (r[m] = x[t + 16 m]) into the part's
 // T row: row[16 m'] = r[h MPP + m'] (h is block-uniform; one unrolled branch
 // per part keeps every register index static)
 // pruned forward row DFT of column part h (input row[16 m'] = x[t + 16 (h MPP + m')])
-template <bool HALF, int NPARTS, class TW, int HH = 0>
+template <int NPARTS, class TW, int HH = 0>
 __device__ __forceinline__ void row_dft_part(const float2 *row, float2 (&v)[16], float2 (&o)[6], float2 *scr,
                                              const TW &wt, int t, int xrd, int h) {
     constexpr int MPP = 16 / NPARTS;
@@ -87,9 +83,9 @@ __device__ __forceinline__ void row_dft_part(const float2 *row, float2 (&v)[16],
             for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
             for (int m = 0; m < MPP; ++m) v[HH * MPP + m] = row[16 * m];
-            dft256_inpart_out6<HALF, NPARTS, HH>(v, o, scr, wt, t, xrd);
+            dft256_inpart_out6<NPARTS, HH>(v, o, scr, wt, t, xrd);
         } else {
-            row_dft_part<HALF, NPARTS, TW, HH + 1>(row, v, o, scr, wt, t, xrd, h);
+            row_dft_part<NPARTS, TW, HH + 1>(row, v, o, scr, wt, t, xrd, h);
         }
     }
 }
@@ -101,8 +97,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     using namespace fz;
     using C = FzCfg<NT>;
     constexpr int NG = C::NG, RPG = C::RPG, NW = C::NW;
-    constexpr bool HALF = C::HALF, PARK = C::PARK;
-    static_assert(KS == 1 || (!PARK && (KS == 2 || KS == 4)), "split mode is NT 512 only");
+    static_assert(KS == 1 || KS == 2 || KS == 4, "one workgroup per patch, or split mode with 2 / 4");
     static_assert(6 * RPG * 16 <= C::XT, "pupil numerators are parked in the group's exchange tile");
     constexpr int NPARTS = n_parts(KS), TH = part_cols(KS), TLD = TH + 1;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
@@ -124,7 +119,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
     // exchange read base (see exchange16 / xchg)
-    const int xrd = HALF ? opaque_int((t & 7) * XP) : exch_rbase(t);
+    const int xrd = exch_rbase(t);
     const int lane = tid & 63, w = tid >> 6;
     // split mode: block k -> patch 8 (k / (8 KS)) + k % 8, part (k / 8) % KS, so
     // the parts of a patch are 8 blocks apart (the same XCD under round-robin
@@ -177,13 +172,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 
     float2 *spec = st.spec + (size_t)b * L * L;
     float2 *pup = st.pupil + (size_t)b * NB * NB;
-    // parking slots of this lane, wave-major [b][w][P 6*RPG | F 6*RPG][64 lanes]:
-    // coalesced 512-B wave accesses, and every slot an immediate offset from
-    // one of two per-lane bases
-    float2 *parkp = a.pscr + ((size_t)(b * NW + w) * 12 * RPG) * 64 + lane;
-    float2 *parkf = parkp + 6 * RPG * 64;
-    auto parkP = [&](int j, int s) -> float2 & { return parkp[(j * 6 + s) * 64]; };
-    auto parkF = [&](int j, int s) -> float2 & { return parkf[(j * 6 + s) * 64]; };
     int kyr[RPG];
     bool ron[RPG];
     float2 P[RPG][6];
@@ -199,17 +187,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             const bool in = ron[j] && (kyr[j] * kyr[j] + kx * kx <= R * R);
             inmask[j] |= (in ? 1u : 0u) << s;
             P[j][s] = in ? pup[(kyr[j] + R) * NB + kx + R] : make_float2(0.f, 0.f);
-            if (PARK) parkP(j, s) = P[j][s];
         }
     }
-    auto loadP = [&]() {
-        if (PARK) {
-#pragma unroll
-            for (int j = 0; j < RPG; ++j)
-#pragma unroll
-                for (int s = 0; s < 6; ++s) P[j][s] = parkP(j, s);
-        }
-    };
     __syncthreads();  // tpx / tky / sig
     // per-lane half-T row offsets of this lane's six column slots; rows
     // outside the box read the zero row `nrows` and write the dummy row after it
@@ -345,9 +324,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             for (int s = 0; s < 6; ++s) Opre[j][s] = ldO(sr, j, s);
         if (towner) Ot = sr[tp.x * L + tp.y];
     }
-#ifdef FPM_PRIO_YOUNG  // A/B: static VALU priority for the second-dispatched half of the waves
-    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
@@ -366,12 +342,11 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll 1
         for (int h = hb; h < he; ++h) {
             // this lane's four-step twiddles W256^{m t}, m = 0..15 (Tw)
-            Tw<!PARK> wt;
+            Tw wt;
             wt.load(tw2, t);
-            // measurement I[t + 16 m2][x] for this lane's pass-B columns; NT
-            // 512 issues the first column before pass A and prefetches one
-            // round ahead inside pass B, NT 1024 loads at the top of each round
-            constexpr int NQ = TH / (4 * NW);
+            // measurement I[t + 16 m2][x] for this lane's pass-B columns,
+            // loaded at the top of each pass-B round (one round ahead measured
+            // 5 % slower: 16 VGPRs the scheduler needs)
             // pass B works on 32 column blocks per half: block r8 gives group gg
             // of a wave column (r8 & 15) + 16 gg + 64 (r8 >> 4)
             constexpr int NBLK = TH / 4;
@@ -382,14 +357,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
             };
-#ifndef FPM_MEAS_PREF
-#define FPM_MEAS_PREF 0  // 1: one round ahead (measured 5% slower: 16 VGPRs the scheduler needs)
-#endif
-            constexpr bool MPREF = FPM_MEAS_PREF && !PARK;  // measurement prefetched one round ahead
-            uint4 nI[2];
-            if (MPREF) ldI(colx(w), nI);  // this wave's first block is block w
             // ---- A: row IDFTs of the box rows, columns [128h, 128h+128) kept
-            loadP();
             float2 X[RPG][6];
 #pragma unroll
             for (int j = 0; j < RPG; ++j)
@@ -402,7 +370,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = X[j][s];
-                idft256_in6<HALF>(v, r, scr, wt, t, xrd);
+                idft256_in6(v, r, scr, wt, t, xrd);
                 // keep the column part h: row[16 m'] = r[h MPP + m'] (one branch
                 // per part keeps every register index static; a shared helper
                 // made the compiler select between addresses of r and put r
@@ -472,62 +440,32 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             // rate while the older one waited at the barrier (stamps: 29.8k vs
             // 44.3k cycles per LED).  The claim for the next block is issued at
             // the top of a round and consumed after the inverse transform.
-            float2 tin[6];
-            if (!PARK) {  // the column's six half-T slots, read one round ahead
+            float2 tin[6];  // the column's six half-T slots, read one round ahead
 #pragma unroll
-                for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(w)];
-            }
+            for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + colx(w)];
             int r8 = w;
 #pragma unroll 1
-            for (int q = 0; PARK ? q < NQ : true; ++q) {
-                const int xl = PARK ? colx(w + NW * q) : colx(r8);
+            for (;;) {
+                const int xl = colx(r8);
                 uint4 cI[2];
                 int nx = 0;
-                if (PARK) {
-#pragma unroll
-                    for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xl];
-                } else {
-                    if (lane == 0) nx = atomicAdd(ccnt, 1);
-                    nx = __builtin_amdgcn_readfirstlane(nx);
-                    if (MPREF) {
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) cI[i] = nI[i];
-                    } else {
-                        ldI(xl, cI);
-                    }
-                }
+                if (lane == 0) nx = atomicAdd(ccnt, 1);
+                nx = __builtin_amdgcn_readfirstlane(nx);
+                ldI(xl, cI);
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) v[SK[s]] = tin[s];
-                if (PARK) ldI(xl, cI);
-                idft256_in6<HALF>(v, r, scr, wt, t, xrd);
-                if (!PARK) {
-                    // next block's measurement and T slots; unconditional (the
-                    // last round re-reads its own column) so the loads are not
-                    // sunk into a branch
+                idft256_in6(v, r, scr, wt, t, xrd);
+                {
+                    // next block's T slots; unconditional (the last round
+                    // re-reads its own column) so the loads are not sunk into
+                    // a branch
                     const int xn = colx(nx < NBLK ? nx : r8);
-                    if (MPREF) ldI(xn, nI);
 #pragma unroll
                     for (int s = 0; s < 6; ++s) tin[s] = th[roff[s] + xn];
                 }
                 const unsigned iw[8] = {cI[0].x, cI[0].y, cI[0].z, cI[0].w, cI[1].x, cI[1].y, cI[1].z, cI[1].w};
-#ifdef FPM_AMP_PIPE  // A/B: software-pipelined (pixel m's v_rsq, then pixel m + 1's eps add and magnitude)
-                {
-                    auto Ipx = [&](int m2) { return (float)((m2 & 1) ? (iw[m2 >> 1] >> 16) : (iw[m2 >> 1] & 0xffffu)); };
-                    auto qof = [&](int m2) {
-                        const pf2 tt = pin(r[m2]) + (pf2){epsn, epsn_im};
-                        return __builtin_fmaf(__builtin_fmaf(tt.x, tt.x, tt.y * tt.y), Ipx(m2), 1.17549435e-38f);
-                    };
-                    float q = qof(0);
-#pragma unroll
-                    for (int m2 = 0; m2 < 16; ++m2) {
-                        const float rs = __builtin_amdgcn_rsqf(q);
-                        if (m2 + 1 < 16) q = qof(m2 + 1);
-                        v[m2] = pout(pin(r[m2]) * (Ipx(m2) * rs));
-                    }
-                }
-#else
 #pragma unroll
                 for (int m2 = 0; m2 < 16; ++m2) {
                     const float Iv = (float)((m2 & 1) ? (iw[m2 >> 1] >> 16) : (iw[m2 >> 1] & 0xffffu));
@@ -539,15 +477,12 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     const float sc = amp_scale(mag2, Iv);
                     v[m2] = pout(pin(r[m2]) * sc);
                 }
-#endif
                 float2 o[6];
-                dft256_out6<HALF>(v, o, scr, wt, t, xrd);
+                dft256_out6(v, o, scr, wt, t, xrd);
 #pragma unroll
                 for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
-                if (!PARK) {
-                    if (nx >= NBLK) break;
-                    r8 = nx;
-                }
+                if (nx >= NBLK) break;
+                r8 = nx;
             }
             FPM_STAMP(10)  // this wave's own columns done
             __syncthreads();
@@ -566,15 +501,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     continue;
                 }
                 float2 o[6];
-                row_dft_part<HALF, NPARTS>(th + (g + NG * j) * TLD + t, v, o, scr, wt, t, xrd, h);
+                row_dft_part<NPARTS>(th + (g + NG * j) * TLD + t, v, o, scr, wt, t, xrd, h);
 #pragma unroll
-                for (int s = 0; s < 6; ++s) F[j][s] = h == hb ? o[s] : cadd(PARK ? parkF(j, s) : F[j][s], o[s]);
-            }
-            if (PARK && h == 0) {  // F is not held through the second half's passes A and B
-#pragma unroll
-                for (int j = 0; j < RPG; ++j)
-#pragma unroll
-                    for (int s = 0; s < 6; ++s) parkF(j, s) = F[j][s];
+                for (int s = 0; s < 6; ++s) F[j][s] = h == hb ? o[s] : cadd(F[j][s], o[s]);
             }
             FPM_STAMP(8)
             // tail pixels: 16 lanes sum the part's TH terms; first half of the waves only
@@ -682,7 +611,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
         if (it > 0) pm = pm_of_red();  // the previous LED's pupil (:415)
-        loadP();
         // Straight-line over all slots: outside the support O = P = 0, so the
         // numerator is exactly 0 and only the spectrum store and the tile
         // bookkeeping need the mask.
@@ -785,7 +713,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 const float2 n = scr[(j * 6 + s) * 16 + t];
                 P[j][s] = make_float2(P[j][s].x + n.x * rom, P[j][s].y + n.y * rom);
                 pmx = fmaxf(pmx, cabs2(P[j][s]));
-                if (PARK) parkP(j, s) = P[j][s];
             }
         if (towner) {
             Pt = make_float2(Pt.x + NPt.x * rom, Pt.y + NPt.y * rom);
@@ -814,7 +741,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     if (hown > 0) return;  // the first part's workgroup owns the per-patch state
 
     // ---- write back the per-patch state
-    loadP();
 #pragma unroll
     for (int j = 0; j < RPG; ++j)
 #pragma unroll
@@ -828,10 +754,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
 
 // ------------------------------------------------------------------ host side
 namespace {
-size_t fused_lds_bytes(int nt, int ks, int nbt, int n_tail_rows) {
-    const int ng = nt / 16, xt = nt > 512 ? 8 * XP : XTILE;
+size_t fused_lds_bytes(int ks, int nbt, int n_tail_rows) {
     const int tld = part_cols(ks) + 1;
-    return (size_t)(ng * xt + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
+    return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
            (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
@@ -840,24 +765,13 @@ size_t fused_lds_bytes(int nt, int ks, int nbt, int n_tail_rows) {
 
 // Threads per workgroup of the fused kernel for this geometry: 512 (2 waves
 // per SIMD), or 0 when its LDS does not fit (fused path unsupported).
-// FPM_FUSED_NT=1024 selects the 4-waves-per-SIMD variant where its LDS fits:
-// measured on MI355X it is SLOWER (14.15 vs 11.67 ms per launch at the metric
-// geometry, profiles/r02_fused_ab.txt): pass B does not speed up with twice
-// the waves (the SIMD's VALU issue, not latency, is what is left), and the
-// half exchange and parked P/F cost extra LDS and scratch traffic.
 int fused_threads(int np, int r, int L, const DevState &st) {
     const FusedGeom g = fused_geometry(np, r);
     if (!g.ok || L % kTile != 0) return 0;
     if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1) return 0;
     const Band bd = band_of(st);
-    const char *e = getenv("FPM_FUSED_NT");
-    if (e && atoi(e) == 1024 && fused_lds_bytes(1024, 1, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 1024;
-    if (fused_lds_bytes(512, 1, bd.nbt, g.n_tail_rows) <= 160 * 1024) return 512;
-    return 0;
+    return fused_lds_bytes(1, bd.nbt, g.n_tail_rows) <= 160 * 1024 ? 512 : 0;
 }
-
-// lane-private parking of P and F (1024-thread variant), float2 elements
-size_t fused_park_elems(int nt, int B) { return nt > 512 ? (size_t)B * 2 * 6 * (fz::NROWS / (nt / 16)) * nt : 1; }
 
 size_t fused_T_elems(int, int, int) { return 1; }  // the intermediate lives in LDS
 
@@ -869,8 +783,8 @@ size_t fused_flag_words(int B, int ks) { return 2 * (size_t)ks * B + 1; }
 // DESIGN.md).  Splitting pays off when one workgroup per patch would leave
 // CUs idle (BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU; a
 // 256-patch field strong-scaled over 4 / 8 GPUs: 64 / 32 per GPU) and needs
-// every block co-resident (the parts wait on each other), which the
-// cooperative launch guarantees or refuses: KS = 4 when 4 B <= CUs, KS = 2
+// every block co-resident (the parts wait on each other; launch_coresident
+// checks the grid against the occupancy query): KS = 4 when 4 B <= CUs, KS = 2
 // when 2 B <= CUs, else 1.  FPM_NO_SPLIT=1 disables it; FPM_SPLIT=1/2/4 forces
 // a part count where the grid still fits.
 int fused_split_parts(int nt, int B, int n_cu) {
@@ -885,11 +799,11 @@ int fused_split_parts(int nt, int B, int n_cu) {
 
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                  float2 *pscr, int nt, int ks, unsigned long long *dbg, float2 *xch, int *flags,
+                                  int ks, unsigned long long *dbg, float2 *xch, int *flags, int stall_led,
                                   hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
-    if (!g.ok || (nt != 512 && nt != 1024)) return hipErrorInvalidValue;
-    if (ks != 1 && (nt != 512 || (ks != 2 && ks != 4) || !xch || !flags)) return hipErrorInvalidValue;
+    if (!g.ok) return hipErrorInvalidValue;
+    if (ks != 1 && ((ks != 2 && ks != 4) || !xch || !flags)) return hipErrorInvalidValue;
     if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
         return hipErrorInvalidValue;
     FusedArgs a;
@@ -899,7 +813,6 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.x0 = x0_dev;
     a.y0 = y0_dev;
     a.tw = tw_np;
-    a.pscr = pscr;
     a.n_order = n_order;
     a.ky_lo = g.ky_lo;
     a.n_fft_rows = g.n_fft_rows;
@@ -928,16 +841,12 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.xch = ks > 1 ? xch : nullptr;
     a.flags = ks > 1 ? flags : nullptr;
     a.abort_flag = ks > 1 ? flags + ks * st.B : nullptr;
-    {
-        const char *e = getenv("FPM_DEBUG_SPLIT_STALL");
-        a.stall_led = e ? atoi(e) : -1;
-    }
-    const size_t lds = fused_lds_bytes(nt, ks, a.nbt, g.n_tail_rows);
+    a.stall_led = ks > 1 ? stall_led : -1;
+    const size_t lds = fused_lds_bytes(ks, a.nbt, g.n_tail_rows);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const void *fn = nt == 1024 ? (const void *)k_fused_iteration<1024, 1>
-                     : ks == 4  ? (const void *)k_fused_iteration<512, 4>
-                     : ks == 2  ? (const void *)k_fused_iteration<512, 2>
-                                : (const void *)k_fused_iteration<512, 1>;
+    const void *fn = ks == 4   ? (const void *)k_fused_iteration<512, 4>
+                     : ks == 2 ? (const void *)k_fused_iteration<512, 2>
+                               : (const void *)k_fused_iteration<512, 1>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (ks > 1) {
@@ -948,13 +857,9 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
         e = hipMemsetAsync(flags, 0, (size_t)ks * st.B * sizeof(int), s);
         if (e == hipSuccess) e = hipMemsetAsync(flags + ks * st.B + 1, 0, (size_t)ks * st.B * sizeof(int), s);
         if (e != hipSuccess) return e;
-        void *args[] = {&a};
-        return hipLaunchCooperativeKernel(fn, dim3(8 * ks * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
+        return launch_coresident(fn, 8 * ks * ((st.B + 7) / 8), 512, lds, &a, s);
     }
-    if (nt == 1024)
-        hipLaunchKernelGGL((k_fused_iteration<1024, 1>), dim3(st.B), dim3(1024), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_fused_iteration<512, 1>), dim3(st.B), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((k_fused_iteration<512, 1>), dim3(st.B), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 

@@ -113,17 +113,11 @@ __device__ __forceinline__ void spec_st(const DevState &st, int b, size_t i, flo
         st.spec[o] = v;
 }
 
-// ePIE update coefficient 1 / ((a + i c) m) for the complex denominators of
-// fpmMain.cpp:417-419 / :469-471 (c = 0 under FPM_FLAG_SCALAR_RE_ONLY),
-// a = |X|^2 + delta >= delta > 0, taken scale-safely (update.hpp): with
-// q = c / a, 1 / ((a + ic) m) = (1 - iq) / (a (1 + q^2) m) -- no |X|^4 term.
-__device__ __forceinline__ float2 upd_coef(float a, float c, float m) {
-    const float ri = __builtin_amdgcn_rcpf(a);
-    const float q = c * ri;
-    const float s = __builtin_amdgcn_rcpf(__builtin_fmaf(q, q, 1.0f) * m) * ri;
-    return make_float2(s, -q * s);
-}
-// IEEE-division variant for the general path
+// ePIE update coefficient 1 / ((a + i c) m) of the general path for the
+// complex denominators of fpmMain.cpp:417-419 / :469-471 (c = 0 under
+// FPM_FLAG_SCALAR_RE_ONLY), a = |X|^2 + delta >= delta > 0, taken
+// scale-safely with IEEE divisions: with q = c / a,
+// 1 / ((a + ic) m) = (1 - iq) / (a (1 + q^2) m) -- no |X|^4 term.
 __device__ __forceinline__ float2 upd_coef_div(float a, float c, float m) {
     const float q = c / a;
     const float d = a * __builtin_fmaf(q, q, 1.0f) * m;

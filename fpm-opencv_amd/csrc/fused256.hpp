@@ -120,51 +120,10 @@ __device__ __forceinline__ void pdft16_inquarter(pf2 (&v)[16], pf2 (&r)[16]) {
     for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
 }
 
-// Exchange of the four-step transforms.  NT = 512: the full 16 x 16 tile per
-// group (dft16.hpp exchange16).  NT = 1024: 64 groups' full tiles (147 KB)
-// do not fit beside the half-T, so each group owns HALF a tile (8 rows, 73.7 KB
-// for all groups) and exchanges in two rounds: every lane writes y[0..7],
-// lanes t < 8 read their row; every lane writes y[8..15], lanes t >= 8 read.
-// The second round's writes may not overtake the first round's reads: LDS
-// operations of one wave execute in issue order, and the laundered read base
-// keeps the compiler from reordering them (see exchange16).
-template <bool HALF>
-__device__ __forceinline__ void xchg(float2 *scr, int t, int xrd, const float2 (&y)[16], float2 (&z)[16]) {
-    if constexpr (!HALF) {
-        exchange16(scr, t, xrd, y, z);
-    } else {
-        const float4 *rp = (const float4 *)(scr + xrd);  // row (t & 7), 16-B aligned (XP even)
-#pragma unroll
-        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[m1];
-        if (t < 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float4 q = rp[j];
-                z[2 * j] = make_float2(q.x, q.y);
-                z[2 * j + 1] = make_float2(q.z, q.w);
-            }
-        }
-#pragma unroll
-        for (int m1 = 0; m1 < 8; ++m1) scr[m1 * XP + t] = y[8 + m1];
-        if (t >= 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float4 q = rp[j];
-                z[2 * j] = make_float2(q.x, q.y);
-                z[2 * j + 1] = make_float2(q.z, q.w);
-            }
-        }
-    }
-}
-
-// Four-step twiddles W256^{m t} (m = 0..15) of lane t: held in 32 VGPRs for a
-// whole half (REG, NT = 512: a table read per use serialised on LDS latency at
-// two waves per SIMD) or read from the LDS table tw2[m][t] at each use (NT =
-// 1024: four waves per SIMD hide the latency, and the registers are needed).
-template <bool REG>
-struct Tw;
-template <>
-struct Tw<true> {
+// Four-step twiddles W256^{m t} (m = 0..15) of lane t, held in 32 VGPRs for a
+// whole pass: a table read per use serialised on LDS latency at two waves per
+// SIMD.
+struct Tw {
     float2 w[16];
     __device__ __forceinline__ void load(const float2 *tw2, int t) {
 #pragma unroll
@@ -172,16 +131,10 @@ struct Tw<true> {
     }
     __device__ __forceinline__ float2 operator[](int m) const { return w[m]; }
 };
-template <>
-struct Tw<false> {
-    const float2 *p;
-    __device__ __forceinline__ void load(const float2 *tw2, int t) { p = tw2 + t; }
-    __device__ __forceinline__ float2 operator[](int m) const { return p[m * 16]; }
-};
 
 // inverse 256-point DFT (unscaled), input v[k] = X[t + 16 k] (only the six
 // SK registers may be non-zero), output r[m2] = x[t + 16 m2]
-template <bool HALF, class TW>
+template <class TW>
 __device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], float2 *scr, const TW &wt, int t,
                                             int xrd) {
     pf2 pv[16], py[16];
@@ -190,14 +143,14 @@ __device__ __forceinline__ void idft256_in6(float2 (&v)[16], float2 (&r)[16], fl
     ptwiddle15<true>(py, wt);
     float2 y[16];
     from_pk(py, y);
-    xchg<HALF>(scr, t, xrd, y, v);
+    exchange16(scr, t, xrd, y, v);
     to_pk(v, pv);
     pdft16<true>(pv, py);
     from_pk(py, r);
 }
 
 // forward 256-point DFT, input v[n2] = x[t + 16 n2], output o[s] = X[t + 16 SK[s]]
-template <bool HALF, class TW>
+template <class TW>
 __device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt, int t,
                                             int xrd) {
     pf2 pv[16], py[16], po[6];
@@ -206,7 +159,7 @@ __device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], flo
     ptwiddle15<false>(py, wt);
     float2 y[16];
     from_pk(py, y);
-    xchg<HALF>(scr, t, xrd, y, v);
+    exchange16(scr, t, xrd, y, v);
     to_pk(v, pv);
     pdft16_out6<false>(pv, po);
     from_pk(po, o);
@@ -214,7 +167,7 @@ __device__ __forceinline__ void dft256_out6(float2 (&v)[16], float2 (&o)[6], flo
 
 // forward 256-point DFT of a half row (x = t + 16 n2, n2 in [8H, 8H+8), zero
 // elsewhere), output o[s] = X[t + 16 SK[s]]
-template <bool HALF, int H, class TW>
+template <int H, class TW>
 __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt, int t,
                                                    int xrd) {
     pf2 pv[16], py[16], po[6];
@@ -223,7 +176,7 @@ __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[
     ptwiddle15<false>(py, wt);
     float2 y[16];
     from_pk(py, y);
-    xchg<HALF>(scr, t, xrd, y, v);
+    exchange16(scr, t, xrd, y, v);
     to_pk(v, pv);
     pdft16_out6<false>(pv, po);
     from_pk(po, o);
@@ -231,11 +184,11 @@ __device__ __forceinline__ void dft256_inhalf_out6(float2 (&v)[16], float2 (&o)[
 
 // forward 256-point DFT of part P of NPARTS (x = t + 16 n2, n2 in
 // [P 16/NPARTS, (P+1) 16/NPARTS), zero elsewhere), output o[s] = X[t + 16 SK[s]]
-template <bool HALF, int NPARTS, int P, class TW>
+template <int NPARTS, int P, class TW>
 __device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[6], float2 *scr, const TW &wt,
                                                    int t, int xrd) {
     if constexpr (NPARTS == 2) {
-        dft256_inhalf_out6<HALF, P>(v, o, scr, wt, t, xrd);
+        dft256_inhalf_out6<P>(v, o, scr, wt, t, xrd);
     } else {
         static_assert(NPARTS == 4, "two or four column parts");
         pf2 pv[16], py[16], po[6];
@@ -244,7 +197,7 @@ __device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[
         ptwiddle15<false>(py, wt);
         float2 y[16];
         from_pk(py, y);
-        xchg<HALF>(scr, t, xrd, y, v);
+        exchange16(scr, t, xrd, y, v);
         to_pk(v, pv);
         pdft16_out6<false>(pv, po);
         from_pk(po, o);

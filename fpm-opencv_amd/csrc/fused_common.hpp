@@ -22,8 +22,6 @@ struct FusedArgs {
     const uint16_t *meas;       // [nS][B][x][t][m2] = I[t + 16 m2][x] (meas_layout, preprocess.hip)
     const int *order, *x0, *y0;
     const float2 *tw;           // exp(-2 pi i k / 256), k < 256
-    float2 *pscr;               // 1024-thread variant: lane-private parking of P and F
-                                // [B][2][6][NT] (registers freed across pass B)
     int n_order;
     int ky_lo, n_fft_rows;      // FFT rows ky_lo .. ky_lo + n_fft_rows - 1 (sigma 0..)
     int n_tail_rows;
@@ -47,7 +45,7 @@ struct FusedArgs {
                                 // then the abort flag, then [B][KS] XCC_ID + 1 of each part
     int *abort_flag;            // a handoff timed out: every workgroup leaves.  Sticky: the
                                 // per-launch reset does not clear it, fpm_run reports it
-    int stall_led;              // FPM_DEBUG_SPLIT_STALL (tests only): the last part stops
+    int stall_led;              // fpm_debug_set_stall (tests only): the last part stops
                                 // publishing from this LED on, forcing the timeout path; -1 off
 };
 
@@ -92,6 +90,24 @@ inline FusedGeom fused_geometry(int np, int r) {
     g.nbp = ((fz::NROWS + g.n_tail_rows) + 3) / 4 * 4;
     g.ok = true;
     return g;
+}
+
+// Plain launch of a grid whose workgroups wait on each other (split and
+// distributed modes): every block must be resident at once.  The grid is
+// checked against the occupancy query -- the check hipLaunchCooperativeKernel
+// makes -- and launched plainly: the same residency (MI355X_MICROARCH.md
+// "coop-launch") without the cooperative launch's per-launch host cost.  Every
+// wait in those kernels also gives up after ~1 s and raises the sticky abort
+// word, so a grid that could not be co-resident fails instead of hanging.
+inline hipError_t launch_coresident(const void *fn, int grid, int block, size_t lds, FusedArgs *a, hipStream_t s) {
+    int dev = 0, n_cu = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
+    if (e != hipSuccess) return e;
+    if ((long long)per_cu * n_cu < grid) return hipErrorCooperativeLaunchTooLarge;
+    void *args[] = {a};
+    return hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s);
 }
 
 struct Band {

@@ -210,9 +210,12 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     };
     int sync_no = 0;  // handoffs of this launch (flag values are 1, 2, 3, ...)
     bool aborted = false;
+    int cur = 0;      // LED position of the handoffs below
     auto handoff = [&]() {
         ++sync_no;
-        handoff_publish(flg + hown, sync_no, local);
+        // fault injection (fpm_debug_set_stall): the last part stops
+        // publishing from LED position stall_led on, its partners time out
+        if (a.stall_led < 0 || cur < a.stall_led || hown != KS - 1) handoff_publish(flg + hown, sync_no, local);
         return handoff_wait<KS>(flg, hown, sync_no, a.abort_flag, ccnt + 1, local, rf);
     };
 
@@ -243,11 +246,12 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     unsigned *tmu = (unsigned *)tmx;
 
     for (int it = 0; it < a.n_order; ++it) {
+        cur = it;
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
         const int wb0 = yc * L + xc;
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
-        Tw<true> wt;
+        Tw wt;
         wt.load(tw2, t);
         float2 v[16], r[16];
 
@@ -260,7 +264,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
             for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
-            idft256_in6<false>(v, r, scr, wt, t, xrd);
+            idft256_in6(v, r, scr, wt, t, xrd);
             if (ron) {
 #pragma unroll
                 for (int m = 0; m < 16; ++m) cst(ra, irow * NP + t + 16 * m, r[m]);
@@ -353,7 +357,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                     for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
                     for (int s = 0; s < 6; ++s) v[SK[s]] = tin[s];
-                    idft256_in6<false>(v, r, scr, wt, t, xrd);
+                    idft256_in6(v, r, scr, wt, t, xrd);
                     {
                         const int xn = colx(nx < NBLK ? nx : r8);
 #pragma unroll
@@ -368,7 +372,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                         v[m2] = pout(pin(r[m2]) * amp_scale(mag2, Iv));
                     }
                     float2 o[6];
-                    dft256_out6<false>(v, o, scr, wt, t, xrd);
+                    dft256_out6(v, o, scr, wt, t, xrd);
 #pragma unroll
                     for (int s = 0; s < 6; ++s) th[roff[s] + (roff[s] == zoff ? TLD : 0) + xl] = o[s];
                     if (nx >= NBLK) break;
@@ -398,7 +402,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (g < NOWN) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) v[m] = ron ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
-            dft256_out6<false>(v, F, scr, wt, t, xrd);
+            dft256_out6(v, F, scr, wt, t, xrd);
         } else {
 #pragma unroll
             for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
@@ -608,7 +612,7 @@ size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
 size_t fused_dist_elems(int B, int ks) { return (size_t)B * dist_patch_elems(ks); }
 
 // Workgroups per patch of the distributed mode: KS = 8 when 8 B <= CUs, 4 when
-// 4 B <= CUs (every part must be co-resident: cooperative launch), else 0 (not
+// 4 B <= CUs (every part must be co-resident: launch_coresident), else 0 (not
 // used).  Measured on MI355X at the metric geometry: 32
 // patches 5.32 ms per iteration (split mode KS 4: 5.66), 64 patches 5.54
 // (split 5.66); at 128 patches the two-part version is SLOWER than split
@@ -629,7 +633,7 @@ int fused_dist_parts(int B, int n_cu, int r, int L) {
 
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, hipStream_t s) {
+                             float2 *area, int *flags, int stall_led, hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
     if (!g.ok || (ks != 2 && ks != 4 && ks != 8) || !area || !flags) return hipErrorInvalidValue;
     if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
@@ -669,7 +673,7 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     a.xch = area;
     a.flags = flags;
     a.abort_flag = flags + ks * st.B;
-    a.stall_led = -1;
+    a.stall_led = stall_led;
     const size_t lds = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const void *fn = ks == 8   ? (const void *)k_fused_dist<8>
@@ -681,8 +685,7 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     e = hipMemsetAsync(flags, 0, (size_t)ks * st.B * sizeof(int), s);
     if (e == hipSuccess) e = hipMemsetAsync(flags + ks * st.B + 1, 0, (size_t)ks * st.B * sizeof(int), s);
     if (e != hipSuccess) return e;
-    void *args[] = {&a};
-    return hipLaunchCooperativeKernel(fn, dim3(8 * ks * ((st.B + 7) / 8)), dim3(512), args, (unsigned)lds, s);
+    return launch_coresident(fn, 8 * ks * ((st.B + 7) / 8), 512, lds, &a, s);
 }
 
 }  // namespace fpm

@@ -423,7 +423,7 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
     a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
     a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
-    a.xt = (mr_lds_bytes(st.nb, a.nbt, fm::kXtFast) <= 160 * 1024 && !getenv("FPM_MR_XT100")) ? fm::kXtFast : fm::XT;
+    a.xt = mr_lds_bytes(st.nb, a.nbt, fm::kXtFast) <= 160 * 1024 ? fm::kXtFast : fm::XT;
     const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xt);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

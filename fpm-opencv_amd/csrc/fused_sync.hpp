@@ -41,9 +41,7 @@ __device__ __forceinline__ int xcc_id() {
     return x & 15;
 }
 __device__ __forceinline__ void handoff_publish(int *flag, int value, bool local) {
-#ifndef FPM_EXP_NOWAIT  // timing experiment only (racy)
     __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are acknowledged
-#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         if (local) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -51,32 +49,42 @@ __device__ __forceinline__ void handoff_publish(int *flag, int value, bool local
     }
 }
 // wait until every other part's flag (flags[0..KS), part `me` excluded) has
-// reached `value`
+// reached `value`.  Lane p < KS of the first wave polls part p's flag and the
+// last lane polls the abort word, all in ONE vector load per spin: one L2 round
+// trip however many partners (a single polling lane walking the partners in
+// turn paid KS - 1 dependent round trips per handoff even when every flag was
+// already set).
 template <int KS>
 __device__ __forceinline__ bool handoff_wait(int *flags, int me, int value, int *abort_flag, int *okslot, bool local,
                                              __amdgpu_buffer_rsrc_t rflag) {
-    if (threadIdx.x == 0) {
+    static_assert(KS < 64, "one polling lane per part");
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        const bool poll = l < KS && l != me, watch = l == 63;
+        bool done = !poll;  // lanes with nothing to wait for
         int ok = 1;
-#pragma unroll
-        for (int p = 0; p < KS; ++p) {
-            if (p == me || !ok) continue;
-            for (int spins = 0;
-                 (local ? ld_l2_i32(rflag, p * (int)sizeof(int))
-                        : __hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < value;
-                 ++spins) {
-                if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    ok = 0;
-                    break;
-                }
-                if (spins > (1 << 23)) {
-                    __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
+        for (int spins = 0;; ++spins) {
+            int f = 0;
+            if (poll && !done)
+                f = local ? ld_l2_i32(rflag, l * (int)sizeof(int))
+                          : __hip_atomic_load(flags + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (watch)
+                f = __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (poll) done = done || f >= value;
+            const bool aborted = __builtin_amdgcn_readlane(watch ? f : 0, 63) != 0;
+            if (__all(done)) break;
+            if (aborted) {
+                ok = 0;
+                break;
             }
+            if (spins > (1 << 23)) {
+                if (l == 0) __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
         }
-        *okslot = ok;
+        if (l == 0) *okslot = ok;
     }
     __syncthreads();
     return *okslot != 0;

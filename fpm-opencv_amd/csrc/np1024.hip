@@ -58,13 +58,8 @@ static_assert(4 * 8 * CXP <= WTILE, "cross-group tile");
 
 // R1 holds its row's loads in registers (hoisted ahead of the pupil stores):
 // 128 VGPRs = 4 waves per SIMD with a few spills (measured 38.5 -> 36.3 us per
-// launch at config 5), or 3 waves without (-DFPM_N1K_OCC3).  The same
+// launch at config 5; 3 waves without the spills measured slower).  The same
 // hoisting in R2 measured slower (36.4 -> 40.0 us) and is not used.
-#ifdef FPM_N1K_OCC3
-#define FPM_N1K_ROWS_OCC
-#else
-#define FPM_N1K_ROWS_OCC __attribute__((amdgpu_waves_per_eu(4)))
-#endif
 
 namespace {
 
@@ -155,7 +150,7 @@ __device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__re
 // K4 left (:460,467), and the row's max|P| for this LED's update (:415) as
 // partial pmax[row] -- the same arithmetic as K5, so the results are
 // bit-identical; K5 itself then runs once, after the last LED.
-__global__ void __launch_bounds__(n1k::NT) FPM_N1K_ROWS_OCC k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw,
+__global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4))) k_rows1024_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw,
                                                           int commit) {
     using namespace n1k;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
@@ -216,7 +211,7 @@ __global__ void __launch_bounds__(n1k::NT) FPM_N1K_ROWS_OCC k_rows1024_inv(DevSt
 }
 
 // C: grid (N / CW, B), block 64 CW: CW adjacent columns, a wave each (CW 8:
-// 64-byte row segments of T per block, the default; 4 / 16 by FPM_N1K_CW)
+// 64-byte row segments of T per block; 4 and 16 measured slower)
 template <int CW>
 __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4))) k_cols1024(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n1k;
@@ -332,25 +327,16 @@ hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const
     if (!np1024_supported(st.np, st.r) || st.meas_g != N || st.npart < st.nb) return hipErrorInvalidValue;
     const size_t lds_r = (size_t)(N + WPB * WTILE) * sizeof(float2);
     // column-pass width: 8 columns per block (64-byte row segments of T;
-    // config 5: 56.5-57.4 vs 58.3-59.1 ms of LED steps with 4), FPM_N1K_CW=4/16
-    const char *cwe = std::getenv("FPM_N1K_CW");
-    const int cwv = cwe ? std::atoi(cwe) : 8;
-    const int cw = cwv == 4 || cwv == 16 ? cwv : 8;
+    // config 5: 56.5-57.4 vs 58.3-59.1 ms of LED steps with 4, 16 slower again)
+    constexpr int cw = 8;
     const size_t strip = std::max((size_t)st.nb * (cw + 1), (size_t)cw * WTILE);
     const size_t lds_c = (N + strip) * sizeof(float2);
-    const void *fc = cw == 16 ? (const void *)k_cols1024<16>
-                     : cw == 8 ? (const void *)k_cols1024<8>
-                               : (const void *)k_cols1024<4>;
+    const void *fc = (const void *)k_cols1024<cw>;
     hipError_t e = hipFuncSetAttribute(fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
     if (e != hipSuccess) return e;
     const dim3 rgrid((st.nb + WPB - 1) / WPB, st.B);
     hipLaunchKernelGGL(k_rows1024_inv, rgrid, dim3(NT), lds_r, s, st, sa, tw, commit ? 1 : 0);
-    if (cw == 16)
-        hipLaunchKernelGGL(k_cols1024<16>, dim3(N / 16, st.B), dim3(1024), lds_c, s, st, sa, tw);
-    else if (cw == 8)
-        hipLaunchKernelGGL(k_cols1024<8>, dim3(N / 8, st.B), dim3(512), lds_c, s, st, sa, tw);
-    else
-        hipLaunchKernelGGL(k_cols1024<4>, dim3(N / 4, st.B), dim3(256), lds_c, s, st, sa, tw);
+    hipLaunchKernelGGL(k_cols1024<cw>, dim3(N / cw, st.B), dim3(64 * cw), lds_c, s, st, sa, tw);
     hipLaunchKernelGGL(k_rows1024_fwd, rgrid, dim3(NT), lds_r, s, st, sa, tw);
     return hipGetLastError();
 }

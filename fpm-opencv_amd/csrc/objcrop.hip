@@ -27,12 +27,6 @@
 #include "dft200.hpp"
 #include "fpm_state.hpp"
 
-#ifndef FPM_CROP_UNROLL
-#define FPM_CROP_UNROLL 4   // strip load/store loop unroll (loads in flight per thread)
-#endif
-#define FPM_CROP_STR_(x) #x
-#define FPM_CROP_STR(x) FPM_CROP_STR_(x)
-#define FPM_CROP_PRAGMA_UNROLL _Pragma(FPM_CROP_STR(unroll FPM_CROP_UNROLL))
 
 namespace fpm {
 
@@ -112,13 +106,8 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
     // the bytes in flight per block), parked in registers until their half's
     // LDS round: objCrop 0.636 -> 0.584 ms per step at the metric config
     // (same box, profiles/r03_ab/crop_preload_ab.txt).  L = 1024 would need
-    // 257 VGPRs for it and keeps the per-half loads (FPM_CROP_NO_PRELOAD
-    // selects them everywhere for A/B runs).
-#ifndef FPM_CROP_NO_PRELOAD
+    // 257 VGPRs for it and keeps the per-half loads.
     constexpr bool PRELOAD = M <= 3;
-#else
-    constexpr bool PRELOAD = false;
-#endif
     constexpr int NLD = PRELOAD ? (H * G2 + NTH - 1) / NTH : 1;
     float4 qh[2][NLD];
     if constexpr (PRELOAD) {
@@ -153,7 +142,7 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
         } else {
             // strip load: consecutive threads take consecutive column pairs of a row
             // (16-byte loads: twice the bytes in flight per load instruction)
-FPM_CROP_PRAGMA_UNROLL
+#pragma unroll 4  // strip load/store loop: loads in flight per thread
             for (int idx = ya * G2 + threadIdx.x; idx < (yb + 1) * G2; idx += NTH) {
                 const int y = idx / G2, cc = 2 * (idx - y * G2);
                 const float4 q = *(const float4 *)(base + (size_t)(y + h * H) * L + cc);
@@ -182,7 +171,7 @@ FPM_CROP_PRAGMA_UNROLL
                 if ((r + 16 * p < 8 * M) == (h == 0))
                     strip[(t + 16 * r + 256 * p - h * H) * SP + g] = cscale(x[p][r], scale);
         __syncthreads();
-FPM_CROP_PRAGMA_UNROLL
+#pragma unroll 4  // strip load/store loop: loads in flight per thread
         for (int idx = threadIdx.x; idx < H * G / 2; idx += NTH) {
             const int y = idx / (G / 2), cc = 2 * (idx - y * (G / 2));
             const float2 p0 = strip[y * SP + cc], p1 = strip[y * SP + cc + 1];
@@ -385,23 +374,17 @@ hipError_t launch_crop600(const DevState &st, float2 *out, const float2 *tw_L, h
 
 }  // namespace
 
-#ifndef FPM_CROP_G
-#define FPM_CROP_G 16   // columns per strip: 128-byte row segments
-#endif
-#ifndef FPM_CROP_GR
-#define FPM_CROP_GR 4   // rows per block in the row pass
-#endif
+constexpr int kCropG = 16;   // columns per strip: 128-byte row segments
+constexpr int kCropGR = 4;   // rows per block in the row pass
 
 // hipErrorNotSupported when L is not 512 / 768 / 1024 / 600 (caller falls back to
 // the mixed-radix batched transform)
 hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
     switch (st.L) {
-        case 512: return launch_crop<2, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
-        case 768: return launch_crop<3, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
-        case 1024: return launch_crop<4, FPM_CROP_GR, FPM_CROP_G>(st, out, tw_L, s);
-        case 600:
-            return getenv("FPM_CROP600_OLD") ? c600::launch_crop600<1, 2, 2>(st, out, tw_L, s)
-                                             : c600::launch_crop600<1, 8, 4>(st, out, tw_L, s);
+        case 512: return launch_crop<2, kCropGR, kCropG>(st, out, tw_L, s);
+        case 768: return launch_crop<3, kCropGR, kCropG>(st, out, tw_L, s);
+        case 1024: return launch_crop<4, kCropGR, kCropG>(st, out, tw_L, s);
+        case 600: return c600::launch_crop600<1, 8, 4>(st, out, tw_L, s);
         default: return hipErrorNotSupported;
     }
 }

@@ -17,25 +17,15 @@ namespace fpm {
 // q = c / a, 1 / ((a + ic) m) = (1 - iq) / (a (1 + q^2) m), so no intermediate
 // exceeds a (the form (a - ic) / ((a^2 + c^2) m) squares a = |O|^2 + d1, i.e.
 // |O|^4, which overflows fp32 once |O| reaches ~3e9).  The real factor |P|
-// (|O|) is folded into the coefficient.  |X| is cmag (the tile maxima's function).
-__device__ __forceinline__ float2 upd_coef_safe(float a, float c, float m, float f) {
-#ifdef FPM_UPD_SQUARED  // A/B only: round 2's (a - ic) / ((a^2 + c^2) m), one rcp, overflows at |X| ~ 3e9
-    const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(a, a, c * c) * m) * f;
-    return make_float2(a * r, -c * r);
-#endif
-    const float ri = __builtin_amdgcn_rcpf(a);
-    const float q = c * ri;
-    const float s = __builtin_amdgcn_rcpf(__builtin_fmaf(q, q, 1.0f) * m) * (ri * f);
-    return make_float2(s, -q * s);
-}
+// (|O|) is folded into the coefficient.  The object and the pupil coefficient
+// are computed side by side: every transcendental is followed by the other
+// chain's independent one instead of its own use (a trans-use hazard wait
+// state each time in the chained order), and never more than two in a row
+// (four in a row measured slower).  Every fused kernel
+// calls this one function; tests/test_gpu_update_coef.py pins it through
+// fpm_debug_slot_update up to |O|^2 + delta1 = 1e30.
 __device__ __forceinline__ float2 slot_update(float2 f, float2 o, float2 p, float pm, const DevState &st,
                                               float2 &num, float &oa) {
-#if !defined(FPM_UPD_CHAIN) && !defined(FPM_UPD_SQUARED)
-    // The same operations as the chain below, the object and the pupil
-    // coefficient computed side by side: every transcendental is followed by
-    // the other chain's independent one instead of its own use (a trans-use
-    // hazard wait state each time in the chained order), and never more than
-    // two in a row (four in a row measured slower).
     const pf2 po = pin(o), pp = pin(p);
     const float pa2 = cabs2(p), oa2 = cabs2(o);
     const float pa = __builtin_amdgcn_sqrtf(pa2);
@@ -51,17 +41,6 @@ __device__ __forceinline__ float2 slot_update(float2 f, float2 o, float2 p, floa
     const float sp = sp0 * fp, so = so0 * fo;
     num = pout(pmul(dq, (pf2){so, -qo * so}));
     return pout(po + pmul(dp, (pf2){sp, -qp * sp}));
-#else
-    const pf2 po = pin(o), pp = pin(p);
-    const pf2 D = pin(f) - pmul(po, pp);
-    const float pa = cmag(p);
-    const float2 cp = upd_coef_safe(__builtin_fmaf(pa, pa, st.delta2), st.d2_im, pm, pa);
-    const pf2 nv = po + pmul(pmulc(D, pp), pin(cp));
-    oa = cmag(o);
-    const float2 co = upd_coef_safe(__builtin_fmaf(oa, oa, st.delta1), st.d1_im, 1.0f, oa);
-    num = pout(pmul(pmulc(D, po), pin(co)));
-    return pout(nv);
-#endif
 }
 
 }  // namespace fpm

@@ -48,10 +48,11 @@ HIP_SYMBOLS = (
     "fpm_init", "fpm_run", "fpm_synchronize", "fpm_download",
     "fpm_download_objcrop_device", "fpm_set_stream", "fpm_get_info",
     "fpm_get_timing", "fpm_runFPM", "fpm_last_error", "fpm_version",
-    "fpm_upload_frames", "fpm_download_stack",
+    "fpm_upload_frames", "fpm_download_stack", "fpm_get_info_sized", "fpm_abi_version",
 )
 # test-only entry points (include/fpm_hip_debug.h)
-HIP_DEBUG_SYMBOLS = ("fpm_debug_update_coef",)
+HIP_DEBUG_SYMBOLS = ("fpm_debug_slot_update", "fpm_debug_update_coef", "fpm_debug_set_stall")
+ABI_VERSION = 4  # include/fpm_hip.h FPM_ABI_VERSION this mirror follows
 
 
 class FpmError(RuntimeError):
@@ -84,7 +85,7 @@ class fpm_frames(C.Structure):
 class fpm_info(C.Structure):
     _fields_ = [("path", C.c_int32), ("box", C.c_int32), ("support_px", C.c_int32),
                 ("device", C.c_int32), ("device_bytes", C.c_size_t), ("wg_per_patch", C.c_int32),
-                ("fused_kernel", C.c_int32)]
+                ("fused_kernel", C.c_int32), ("threads_per_wg", C.c_int32)]
 
 
 class fpm_timing(C.Structure):
@@ -120,6 +121,9 @@ def load_library(path: str = HIP_LIB):
         "fpm_download_objcrop_device": (C.c_int, [vp, vp]),
         "fpm_set_stream": (C.c_int, [vp, vp]),
         "fpm_get_info": (C.c_int, [vp, C.POINTER(fpm_info)]),
+        "fpm_get_info_sized": (C.c_int, [vp, C.POINTER(fpm_info), C.c_size_t]),
+        "fpm_abi_version": (C.c_int, []),
+        "fpm_debug_set_stall": (C.c_int, [vp, C.c_int]),
         "fpm_get_timing": (C.c_int, [vp, C.POINTER(fpm_timing)]),
         "fpm_runFPM": (C.c_int, [C.POINTER(fpm_problem), C.c_int, u16p, C.c_int,
                                  f32p, f32p, f32p, f32p]),
@@ -132,6 +136,8 @@ def load_library(path: str = HIP_LIB):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.fpm_abi_version() != ABI_VERSION:
+        raise OSError(f"{path}: ABI {lib.fpm_abi_version()}, this mirror follows ABI {ABI_VERSION}: rebuild")
     _lib = lib
     return lib
 
@@ -289,8 +295,14 @@ class Solver:
 
     def info(self) -> fpm_info:
         i = fpm_info()
-        _check(_lib.fpm_get_info(self._h, C.byref(i)))
+        _check(_lib.fpm_get_info_sized(self._h, C.byref(i), C.sizeof(i)))
         return i
+
+    def debug_set_stall(self, led: int):
+        """Test-only fault injection (include/fpm_hip_debug.h): from LED
+        position `led` on, the last workgroup of each patch stops publishing
+        its split / distributed-mode handoffs; -1 switches it off."""
+        _check(_lib.fpm_debug_set_stall(self._h, int(led)))
 
     def timing(self) -> fpm_timing:
         t = fpm_timing()

@@ -29,6 +29,11 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header.  Round 4 (4): fpm_info gained threads_per_wg;
+ * fpm_get_info_sized lets a caller built against an older header pass its
+ * smaller struct.  fpm_abi_version() reports the library's revision. */
+#define FPM_ABI_VERSION   4
+
 #define FPM_OK            0
 #define FPM_ERR_INVAL   (-22)   /* bad argument / unsupported geometry      */
 #define FPM_ERR_NOMEM   (-12)   /* device or host allocation failed          */
@@ -135,6 +140,7 @@ typedef struct fpm_info {
                               4 / 8 in split or distributed mode when
                               wg_per_patch * n_patch <= CUs)                   */
     int32_t fused_kernel;  /* FPM_KERNEL_*                                      */
+    int32_t threads_per_wg;/* threads per workgroup of the LED-update kernel (ABI 4) */
 } fpm_info;
 
 /* Per-kernel timing of the most recent fpm_run, from HIP events recorded on
@@ -194,7 +200,11 @@ int  fpm_download_objcrop_device(fpm_ctx *ctx, float *dst_dev);
 /* Use a caller-provided hipStream_t (NULL = the context's own stream). */
 int  fpm_set_stream(fpm_ctx *ctx, void *hip_stream);
 
+/* fpm_get_info fills the fpm_info of THIS header; fpm_get_info_sized writes
+ * only the first info_size bytes (pass sizeof(fpm_info) of the header the
+ * caller was built with: fields are only ever appended). */
 int  fpm_get_info(const fpm_ctx *ctx, fpm_info *info);
+int  fpm_get_info_sized(const fpm_ctx *ctx, fpm_info *info, size_t info_size);
 int  fpm_get_timing(const fpm_ctx *ctx, fpm_timing *timing);
 
 /* One-shot equivalent of runFPM for n_patch patches: create, upload, init,
@@ -208,6 +218,9 @@ const char *fpm_last_error(void);
 
 /* Library build identification (also proves the .so loaded). */
 const char *fpm_version(void);
+/* FPM_ABI_VERSION the library was built with; a caller compiled against a
+ * newer header than the library refuses to run. */
+int fpm_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,7 @@ flags (BASELINE config 4: 1024 patches over 8 GPUs = 128 per GPU; the
   * KS = 4 sums four quarter partials ((F_0 + F_1) + F_2) + F_3: the same
     arithmetic up to fp32 rounding (measured rel. L2 vs KS = 1 stated in the
     assertion), deterministic run to run, and checked against the fp64 oracle.
-  * A handoff that times out (forced with FPM_DEBUG_SPLIT_STALL) fails fpm_run
+  * A handoff that times out (forced with fpm_debug_set_stall) fails fpm_run
     even when it happens in an earlier iteration of a multi-iteration run, and
     the context must be re-initialised.
 """
@@ -143,30 +143,35 @@ def test_distributed_matches_one_workgroup_and_oracle(r, nside, step, B, iters, 
             assert rel_l2(outd[k][b], ref[k]) < tol, (k, b)
 
 
-def test_split_handoff_timeout_is_reported_and_sticky():
-    """The last part stops publishing at LED 3 of the first iteration: its
-    partners time out (~seconds), the abort word stays set through the second
-    launch of fpm_run(2), the run fails with FPM_ERR_DEVICE, and the context
-    needs fpm_init again (after which a clean run succeeds)."""
+@pytest.mark.parametrize("dist", [False, True], ids=["split4", "dist8"])
+def test_handoff_timeout_is_reported_and_sticky(dist):
+    """The last part stops publishing at LED 3 of the first iteration
+    (fpm_debug_set_stall): its partners time out (~seconds), the abort word
+    stays set through the second launch of fpm_run(2), the run fails with
+    FPM_ERR_DEVICE, and the context needs fpm_init again (after which a clean
+    run succeeds).  Split mode (4 parts) and the distributed mode (8 parts,
+    three handoffs per LED) both."""
     Np, L, r = 256, 512, 10
     x0, y0, order = grid_geometry(Np, L, 3, 24)
     stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=3)
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=1, path=fpm_amd.PATH_FUSED)
-    os.environ["FPM_NO_DIST"] = "1"  # split mode carries the stall knob
+    env = {"FPM_DIST": "8"} if dist else {"FPM_NO_DIST": "1"}
+    os.environ.update(env)
     try:
         s = fpm_amd.Solver(prob)
     finally:
-        os.environ.pop("FPM_NO_DIST", None)
+        for k in env:
+            os.environ.pop(k, None)
     with s:
-        assert s.info().wg_per_patch == 4
+        info = s.info()
+        assert info.wg_per_patch == (8 if dist else 4)
+        assert info.fused_kernel == (fpm_amd.KERNEL_FUSED_NP256_DIST if dist else fpm_amd.KERNEL_FUSED_NP256)
         s.upload(stack)
         s.init()
-        os.environ["FPM_DEBUG_SPLIT_STALL"] = "3"
-        try:
-            with pytest.raises(fpm_amd.FpmError) as e:
-                s.run(2)
-        finally:
-            os.environ.pop("FPM_DEBUG_SPLIT_STALL", None)
+        s.debug_set_stall(3)
+        with pytest.raises(fpm_amd.FpmError) as e:
+            s.run(2)
+        s.debug_set_stall(-1)
         assert e.value.code == fpm_amd.FPM_ERR_DEVICE
         assert "timed out" in str(e.value)
         with pytest.raises(fpm_amd.FpmError) as e2:  # state is undefined until re-initialised
