@@ -759,7 +759,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         const char *names_f[kStamps] = {"gather", "A:tail+sync", "B:columns", "C:tail+sync", "upd:sync+Opre", "max",
                                         "P",      "A:rowIDFT",   "C:rowDFT",  "upd:body",    "B:loop",
                                         "split:Fstores", "split:Fwait"};
-        const char *names_d[kStamps] = {"gather", "A", "-", "B+Tg", "sync1", "C", "update", "sync2",
+        const char *names_d[kStamps] = {"gather", "A", "sync1", "B", "sync2", "C", "update", "sync3",
                                         "merge+Opre", "max", "P", "-", "-"};
         const char *const *names = c->dist ? names_d : names_f;
         for (int v = 0; v < 2; ++v) {

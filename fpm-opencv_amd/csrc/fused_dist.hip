@@ -5,43 +5,37 @@
 // strictly sequential, fpmMain.cpp:345-476, so only intra-patch parallelism
 // can fill the chip).
 //
-// Two handoffs per LED (round 4; round 3's version had three):
+// Split mode (fpm_fused.hip) gives each workgroup a column part but keeps the
+// row passes and the object/pupil update redundant in every workgroup; here
+// every phase is partitioned, at the price of three handoffs per LED:
 //
-//   every part holds the WHOLE pupil P and the pre-update window O (group g
-//   the FFT rows 2g, 2g + 1; thread i < #tail the tail pixel i), so the row
-//   IDFTs need nothing from the partners; part p owns the column part
-//   [p 256/KS, (p+1) 256/KS) and the FFT rows rho = p (mod KS) (one per
-//   owning group), tail rows q = p (mod KS).
-//   gather   X = O P on the support, all rows                        (:358-364)
-//   A        row IDFTs of ALL box rows, only the own columns kept -> LDS
-//            (redundant in every part: no handoff between A and B)     (:365)
-//   B        own columns: column IDFT, 1/Np^2, amplitude replacement,
-//            column DFT (pass B of fpm_fused.hip verbatim), box rows of
-//            the own columns -> Tg (a per-patch T image in L2-resident
-//            global memory)                                            (:365-394)
-//   sync 1
-//   C        row DFTs of the own rows from Tg (full input), pruned to the
-//            support columns -> F complete, no partial sums            (:394)
-//   update   object update of the own rows on the support (:405-447), pupil
-//            numerator (:457-464) published, tile maxima of |spec| in LDS,
-//            the window's tiles published
+//   part p owns FFT rows i = p, p + KS, p + 2 KS, ... of the 64 (one per
+//   16-lane group), tail rows q = p (mod KS), and the column part
+//   [p 256/KS, (p+1) 256/KS).
+//   gather   O = spec (own rows, on the support), X = O P              (:358-364)
+//   A        row IDFTs of the own rows, all 256 outputs -> Tg (a per-patch
+//            T image in L2-resident global memory)                      (:365)
+//   sync 1   (also carries each part's max|P| partial of the previous LED)
+//   B        Tg[box rows][own columns] -> LDS, column IDFT, 1/Np^2,
+//            amplitude replacement, column DFT (pass B of fpm_fused.hip
+//            verbatim), box rows back to Tg                              (:365-394)
 //   sync 2
-//   merge    next window O of all rows (partners' spectrum writes), partner
-//            numerators, partner window tiles: every part ends with the same
-//            tile maxima, dirty bits and numerators
+//   C        row DFTs of the own rows from Tg (full input), pruned to the
+//            support columns -> F complete, no partial sums               (:394)
+//   update   object update of the own rows on the support (:405-447), pupil
+//            numerator (:457-464), tile maxima of |spec| in LDS
+//   sync 3   (carries the window's tile maxima / dirty bits)
+//   merge    every part folds the partners' window tiles into its LDS copy,
+//            so all parts hold identical tile maxima
 //   max      exact max|objF| (:460,467), redundant in every part (identical)
-//   P        P += num / max|objF| on ALL rows (:468-475) and max|P| (:415),
-//            identical in every part
+//   P        P += num / max|objF| on the own rows (:468-475), max|P| partial
 //
-// Handoffs: one monotone flag per part (2 per LED), all partner flags polled
-// by one vector load (fused_sync.hpp); Tg, the numerators, the tile
+// Handoffs: one monotone flag per part (3 per LED); Tg, the tile
 // publications and the spectrum move with device-coherent policies (plain
 // stores + L1-bypassing loads when every part of the patch sits on one XCD --
-// the L2 is the coherence point -- sc1 otherwise).  No double buffering: a
-// part writes Tg / the numerators / its tiles of LED it + 1 only after sync 1
-// of LED it + 1, which every partner publishes after it has read the LED-it
-// data (C reads Tg before sync 2; the merge reads the numerators and tiles
-// before the next LED's sync 1).
+// the L2 is the coherence point -- sc1 otherwise), see fused_sync.hpp.
+// Tg needs no double buffering: in A and C a part touches only its own rows,
+// in B only its own columns, and every phase change is behind a handoff.
 #include <hip/hip_runtime.h>
 
 #include "dft16.hpp"
@@ -56,28 +50,9 @@ namespace fpm {
 namespace {
 constexpr int kTgRows = fz::NROWS + fz::MAXTAILROWS;  // Tg rows: 64 FFT rows + tail rows
 constexpr int kWinTiles = 64;                         // window tiles published per part (<= 6 x 6 used)
-constexpr int kNumElems = fz::NROWS * 96 + fz::MAXTAIL;  // pupil numerators: [row][slot][t] + tail pixels
-// per-patch distributed-mode area (float2): Tg, KS x kWinTiles tile
-// publications (max, dirty flag), the pupil numerators
-constexpr size_t dist_patch_elems(int ks) { return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + kNumElems; }
-
-// keep the column part h of a row IDFT (r[m] = x[t + 16 m]) in the part's T
-// row: row[16 m'] = r[h MPP + m'].  The part is selected by uniform
-// conditional moves: with one branch per part the compiler merged the
-// branches into one dynamically indexed read of r and put r in scratch.
-template <int KS>
-__device__ __forceinline__ void keep_part(float2 *row, const float2 (&r)[16], int h) {
-    constexpr int MPP = 16 / KS;
-    float2 k[MPP];
-#pragma unroll
-    for (int m = 0; m < MPP; ++m) k[m] = r[m];
-#pragma unroll
-    for (int hh = 1; hh < KS; ++hh)
-#pragma unroll
-        for (int m = 0; m < MPP; ++m) k[m] = h == hh ? r[hh * MPP + m] : k[m];
-#pragma unroll
-    for (int m = 0; m < MPP; ++m) row[16 * m] = k[m];
-}
+// per-patch distributed-mode area (float2): Tg, then KS x kWinTiles tile
+// publications (max, dirty flag), then KS max|P| partials
+constexpr size_t dist_patch_elems(int ks) { return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + ks; }
 }  // namespace
 
 template <int KS>
@@ -85,6 +60,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     using namespace fz;
     constexpr int NT = 512, NG = 32, NW = 8;
     constexpr int TH = NP / KS, TLD = TH + 1;          // own column part
+    constexpr int NOWN = NROWS / KS;                   // own FFT row slots (groups 0 .. NOWN-1)
     constexpr int CB = TH / 4 < 16 ? TH / 4 : 16;      // pass-B block: columns (r8 % CB) + CB gg + 4 CB (r8 / CB)
     constexpr int NBLK = TH / 4;
     static_assert(KS == 2 || KS == 4 || KS == 8, "two, four or eight parts");
@@ -119,7 +95,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * XTILE;
     const int nwords = (a.nbt + 31) >> 5;
-    constexpr int TILES_OFF = kTgRows * NP, NUM_OFF = TILES_OFF + KS * kWinTiles, NUMT_OFF = NUM_OFF + NROWS * 96;
+    constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
 
     // ---- one-time setup
     if (tid == 0) {
@@ -160,30 +136,19 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 
     float2 *spec = st.spec + (size_t)b * L * L;
     float2 *pup = st.pupil + (size_t)b * NB * NB;
-    // FFT rows 2g + j of this group, all parts; the own row (C and the
-    // update) is 2g + jo when 2g + jo = hown (mod KS): KS is even, so jo is
-    // the part's parity and the owning groups are those with 2g = hown - jo
-    const int jo = hown & 1;
-    const bool cgrp = ((2 * g) % KS) == hown - jo;
-    int kyr[2];
-    bool ron[2];
-    float2 P[2][6];
-    unsigned inmask[2];
+    // own FFT row of this group: i = hown + KS g
+    const int irow = hown + KS * g;
+    const int kyr = a.ky_lo + irow;
+    const bool ron = g < NOWN && irow < a.n_fft_rows;
+    float2 P[6];
+    unsigned inmask = 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        kyr[j] = a.ky_lo + 2 * g + j;
-        ron[j] = 2 * g + j < a.n_fft_rows;
-        inmask[j] = 0;
-#pragma unroll
-        for (int s = 0; s < 6; ++s) {
-            const int kx = slot_kx(t, s);
-            const bool in = ron[j] && (kyr[j] * kyr[j] + kx * kx <= R * R);
-            inmask[j] |= (in ? 1u : 0u) << s;
-            P[j][s] = in ? pup[(kyr[j] + R) * NB + kx + R] : make_float2(0.f, 0.f);
-        }
+    for (int s = 0; s < 6; ++s) {
+        const int kx = slot_kx(t, s);
+        const bool in = ron && (kyr * kyr + kx * kx <= R * R);
+        inmask |= (in ? 1u : 0u) << s;
+        P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
-    const int irow = 2 * g + jo;                    // own FFT row of an owning group
-    const bool ron_o = cgrp && ron[jo];
     __syncthreads();  // tpx / tpq / sig
     const int zoff = nrows * TLD;
     int roff[6];
@@ -193,14 +158,13 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         roff[s] = sg >= 0 ? sg * TLD : zoff;
     }
     for (int i = tid; i < TLD; i += NT) th[zoff + i] = make_float2(0.f, 0.f);
-    // tail pixel tid: every part holds it; the part owning its row q = tpq[tid]
-    // (q = hown mod KS) updates it
-    const bool thold = tid < a.n_tail_px;
-    const bool towner = thold && (tpq[tid] % KS) == hown;
-    const int2 tp = thold ? tpx[tid] : make_int2(0, 0);
-    float2 Pt = thold ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
+    // tail pixel tid: this part owns it when its row q = tpq[tid] is q = hown (mod KS)
+    const bool towner = tid < a.n_tail_px && (tpq[tid] % KS) == hown;
+    const int2 tp = tid < a.n_tail_px ? tpx[tid] : make_int2(0, 0);
+    float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
     float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
     float pm = st.pmax[b];
+    float pmx_part = 0.f;  // this part's max|P|^2 of the last pupil phase
 
     // ---- coherence of the patch's shared data (see fused_sync.hpp)
     bool local = false;
@@ -269,23 +233,17 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         const int ln = a.order[itn];
         return (a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2;
     };
-    float2 Opre[2][6];
-    // the whole window on the support (every part); partners' writes are
-    // visible after sync 2 (sc1 loads)
+    float2 Opre[6];
     auto load_window = [&](int itn) {
-        const int wb = wbase(itn);
+        const int wb = wbase(itn) + kyr * L + t;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int s = 0; s < 6; ++s)
-                Opre[j][s] = ((inmask[j] >> s) & 1) ? cld(rs, wb + kyr[j] * L + t + soff(s)) : make_float2(0.f, 0.f);
-        if (thold) Ot = cld(rs, wb + tp.x * L + tp.y);
+        for (int s = 0; s < 6; ++s) Opre[s] = ((inmask >> s) & 1) ? cld(rs, wb + soff(s)) : make_float2(0.f, 0.f);
+        if (towner) Ot = cld(rs, wbase(itn) + tp.x * L + tp.y);
     };
     if (a.n_order > 0) load_window(0);
     const float epsn = st.eps * (float)(NP * NP);
     const float epsn_im = st.eps_im * (float)(NP * NP);
     unsigned *tmu = (unsigned *)tmx;
-    bool pupil_done = false;  // red[32..] holds a pupil phase's maxima
 
     for (int it = 0; it < a.n_order; ++it) {
         cur = it;
@@ -297,54 +255,84 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         wt.load(tw2, t);
         float2 v[16], r[16];
 
-        // ---- gather + A: row IDFTs of all box rows, own columns kept (:358-365)
-        if (thold) tailX[tid] = pout(pmul(pin(Ot), pin(Pt)));
-        __syncthreads();  // tailX; the previous LED's max|P| partials in red[32..]
-        if (pupil_done) {  // max|P| of the previous LED's pupil (:415), identical in every part
-            float pm2 = red[32];
-#pragma unroll
-            for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
-            pm = sqrtf(pm2);
-        }
+        // ---- gather + A: row IDFTs of the own rows, all 256 outputs to Tg (:358-365)
+        if (towner) tailX[tid] = pout(pmul(pin(Ot), pin(Pt)));
+        __syncthreads();  // tailX
         FPM_STAMP(0)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            if (!ron[j]) continue;
+        if (g < NOWN) {  // group-uniform
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[j][s]), pin(P[j][s])));   // :364
+            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
             idft256_in6(v, r, scr, wt, t, xrd);
-            keep_part<KS>(th + (2 * g + j) * TLD + t, r, hown);
-        }
-        // only the own row's pre-update O is needed past pass A (the update);
-        // the other row's registers are free through pass B
-        float2 Oown[6];
+            if (ron) {
 #pragma unroll
-        for (int s = 0; s < 6; ++s) Oown[s] = jo ? Opre[1][s] : Opre[0][s];
-        // tail rows: direct sums over the row's pixels for the own columns
-        for (int idx = tid; idx < a.n_tail_rows * TH; idx += NT) {
-            const int q = idx / TH, xl = idx - q * TH, x = xl + TH * hown;
-            const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
-            const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
-            pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
-            const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
-            pf2 s2 = {0.f, 0.f}, s3 = {0.f, 0.f};
-            int p = 0;
-            for (; p + 1 < np_; p += 2) {
-                s2 += pmulc(pin(tailX[p0 + p]), wa);
-                s3 += pmulc(pin(tailX[p0 + p + 1]), wb);
-                wa = pmul(wa, wstep);
-                wb = pmul(wb, wstep);
+                for (int m = 0; m < 16; ++m) cst(ra, irow * NP + t + 16 * m, r[m]);
             }
-            if (p < np_) s2 += pmulc(pin(tailX[p0 + p]), wa);
-            th[(NROWS + q) * TLD + xl] = pout(s2 + s3);
+        }
+        // own tail rows: direct sums over the row's pixels for every column x
+        for (int q = hown; q < a.n_tail_rows; q += KS) {
+            const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
+            for (int x = tid; x < NP; x += NT) {
+                const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
+                pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
+                const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
+                pf2 s2 = {0.f, 0.f}, s3 = {0.f, 0.f};
+                int p = 0;
+                for (; p + 1 < np_; p += 2) {
+                    s2 += pmulc(pin(tailX[p0 + p]), wa);
+                    s3 += pmulc(pin(tailX[p0 + p + 1]), wb);
+                    wa = pmul(wa, wstep);
+                    wb = pmul(wb, wstep);
+                }
+                if (p < np_) s2 += pmulc(pin(tailX[p0 + p]), wa);
+                cst(ra, (NROWS + q) * NP + x, pout(s2 + s3));
+            }
+        }
+        FPM_STAMP(1)
+        // ---- sync 1, with this part's max|P| partial of the previous LED
+        if (it > 0 && tid == 0) {
+            float m2 = red[32];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) m2 = fmaxf(m2, red[32 + i]);
+            cst(ra, PMX_OFF + hown, make_float2(m2, 0.f));
+        }
+        if (!handoff()) {
+            aborted = true;
+            break;
+        }
+        if (it > 0) {  // max|P| of the previous LED's pupil over all parts (:415)
+            float m2 = 0.f;
+#pragma unroll
+            for (int p = 0; p < KS; ++p) m2 = fmaxf(m2, cld(ra, PMX_OFF + p).x);
+            pm = sqrtf(m2);
+        }
+        FPM_STAMP(2)
+
+        // ---- B: own columns of T from Tg, column IDFT, amplitude, DFT (:365-394)
+        {   // 16-byte loads, all issued before the first LDS write (one L2
+            // round trip, not one per row: the per-row loop measured 13k cycles)
+            constexpr int NQ2 = TH / 2, NLD = (kTgRows * NQ2 + NT - 1) / NT;
+            typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+            u32x4_t q[NLD];
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int i = tid + NT * k, row = i / NQ2, c2 = i - row * NQ2;
+                q[k] = i < nrows * NQ2 ? __builtin_amdgcn_raw_buffer_load_b128(
+                                             ra, (row * NP + TH * hown + 2 * c2) * (int)sizeof(float2), 0, 16)
+                                       : (u32x4_t){0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int i = tid + NT * k, row = i / NQ2, c2 = i - row * NQ2;
+                if (i < nrows * NQ2) {
+                    th[row * TLD + 2 * c2] = make_float2(__uint_as_float(q[k].x), __uint_as_float(q[k].y));
+                    th[row * TLD + 2 * c2 + 1] = make_float2(__uint_as_float(q[k].z), __uint_as_float(q[k].w));
+                }
+            }
         }
         if (tid == 0) *ccnt = NW;
-        __syncthreads();  // own columns of T complete
-        FPM_STAMP(1)
-
-        // ---- B: own columns, column IDFT, amplitude, DFT (:365-394)
+        __syncthreads();
         {
             auto colx = [&](int r8) { return (r8 % CB) + CB * gg + 4 * CB * (r8 / CB); };
             auto ldI = [&](int xl, uint4 (&n)[2]) {
@@ -393,7 +381,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             }
         }
         __syncthreads();
-        for (int i = tid; i < nrows * (TH / 2); i += NT) {  // 16-byte stores of the own columns -> Tg
+        for (int i = tid; i < nrows * (TH / 2); i += NT) {  // 16-byte stores
             const int row = i / (TH / 2), c2 = i - row * (TH / 2);
             const float2 e0 = th[row * TLD + 2 * c2], e1 = th[row * TLD + 2 * c2 + 1];
             typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -403,7 +391,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             else __builtin_amdgcn_raw_buffer_store_b128(d, ra, off, 0, 16);
         }
         FPM_STAMP(3)
-        if (!handoff()) {  // ---- sync 1
+        if (!handoff()) {  // ---- sync 2
             aborted = true;
             break;
         }
@@ -411,9 +399,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 
         // ---- C: row DFTs of the own rows (full input) -> F (:394)
         float2 F[6];
-        if (cgrp) {
+        if (g < NOWN) {
 #pragma unroll
-            for (int m = 0; m < 16; ++m) v[m] = ron_o ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
+            for (int m = 0; m < 16; ++m) v[m] = ron ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
             dft256_out6(v, F, scr, wt, t, xrd);
         } else {
 #pragma unroll
@@ -450,26 +438,22 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
-        if (ron_o) {
-            const unsigned mk = jo ? inmask[1] : inmask[0];
+        if (ron) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
                 float2 num;
                 float oa;
-                const float2 Pj = jo ? P[1][s] : P[0][s];  // jo is block-uniform
-                const float2 nv = slot_update(F[s], Oown[s], Pj, pm, st, num, oa);
-                scr[s * 16 + t] = num;                               // own numerator, this LED's P phase
-                cst(ra, NUM_OFF + (irow * 6 + s) * 16 + t, num);     // the partners'
-                if ((mk >> s) & 1) {
-                    cst(rs, wb0 + (a.ky_lo + irow) * L + t + soff(s), nv);
-                    note(yc + a.ky_lo + irow, xc + slot_kx(t, s), oa, cmag(nv));
+                const float2 nv = slot_update(F[s], Opre[s], P[s], pm, st, num, oa);
+                scr[s * 16 + t] = num;
+                if ((inmask >> s) & 1) {
+                    cst(rs, wb0 + kyr * L + t + soff(s), nv);
+                    note(yc + kyr, xc + slot_kx(t, s), oa, cmag(nv));
                 }
             }
         }
         if (towner) {
             float oa;
             const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
-            cst(ra, NUMT_OFF + tid, NPt);
             cst(rs, wb0 + tp.x * L + tp.y, nv);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
@@ -487,27 +471,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 make_float2(tmx[bk], __uint_as_float((dirty[bk >> 5] >> (bk & 31)) & 1u)));
         }
         FPM_STAMP(6)
-        if (!handoff()) {  // ---- sync 2
+        if (!handoff()) {  // ---- sync 3
             aborted = true;
             break;
         }
         FPM_STAMP(7)
-        // the next window (all rows: partners' spectrum writes are visible),
-        // the partners' numerators and window tiles; every part ends with the
-        // same maxima, dirty bits and numerators
-        if (it + 1 < a.n_order) load_window(it + 1);
-        // partner numerators parked in this group's exchange tile behind the
-        // own row's (slots 96 + (6 j + s) 16 + t; the tile is free until the
-        // next LED's pass A) so they hold no registers through the max phase
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const bool mine = ron_o && j == jo;  // own row: the numerator is in scr
-#pragma unroll
-            for (int s = 0; s < 6; ++s)
-                if (!mine && ((inmask[j] >> s) & 1))
-                    scr[96 + (j * 6 + s) * 16 + t] = cld(ra, NUM_OFF + ((2 * g + j) * 6 + s) * 16 + t);
-        }
-        if (thold && !towner) NPt = cld(ra, NUMT_OFF + tid);
+        // the next window first (its loads overlap the merge), then the
+        // merge: every part ends with the same maxima and dirty bits
+        if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
         if (tid < wnt) {
             const int bk = wtile(tid);
             float m = tmx[bk];
@@ -577,54 +548,56 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         FPM_STAMP(9)
         const float rom = 1.0f / omax;
-        // ---- P += num / max|objF| on ALL rows (:468-475), max|P| (:415):
-        // the same numerators and maximum in every part, so the same P
+        // ---- P += num / max|objF| on the own rows (:468-475), max|P| partial (:415)
         float pmx = 0.f;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
+        if (ron) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                const bool in = (inmask[j] >> s) & 1;
-                const float2 n = (ron_o && j == jo) ? scr[s * 16 + t]
-                                 : in               ? scr[96 + (j * 6 + s) * 16 + t]
-                                                    : make_float2(0.f, 0.f);
-                P[j][s] = make_float2(P[j][s].x + n.x * rom, P[j][s].y + n.y * rom);
-                pmx = fmaxf(pmx, cabs2(P[j][s]));
+                const float2 n = scr[s * 16 + t];
+                P[s] = make_float2(P[s].x + n.x * rom, P[s].y + n.y * rom);
+                pmx = fmaxf(pmx, cabs2(P[s]));
             }
-        if (thold) {
+        }
+        if (towner) {
             Pt = make_float2(Pt.x + NPt.x * rom, Pt.y + NPt.y * rom);
             pmx = fmaxf(pmx, cabs2(Pt));
         }
-        // red[32..] is read after the next LED's first barrier (not used by
-        // the max phase); the numerators in scr are read above by this thread
-        // only and next rewritten after two barriers
         pmx = wave_max(pmx);
         if (lane == 0) red[32 + w] = pmx;
-        pupil_done = true;
         FPM_STAMP(10)
     }
 #undef FPM_STAMP
     __syncthreads();  // red[32..]
-    if (pupil_done) {
-        float pm2 = red[32];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) pm2 = fmaxf(pm2, red[32 + i]);
-        pm = sqrtf(pm2);
-    }
     if (a.dbg && tid == 0 && (hown == 0 || hown == KS - 1))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(hown ? kStamps : 0) + i], acc[i]);
-    // ---- write back: part 0 holds the same pupil, tile maxima and max|P| as
-    // every other part
-    if (hown != 0 || aborted) return;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
+    // ---- write back: each part its own pupil rows and tail pixels; part 0
+    // the tile maxima (identical in every part) and max|P| over all parts
+    if (ron) {
 #pragma unroll
         for (int s = 0; s < 6; ++s)
-            if ((inmask[j] >> s) & 1) pup[(kyr[j] + R) * NB + slot_kx(t, s) + R] = P[j][s];
-    if (thold) pup[(tp.x + R) * NB + tp.y + R] = Pt;
-    for (int k = tid; k < a.nbt; k += NT) tmax_g[band_gtile(k)] = tmx[k];
-    for (int i = tid; i < nwords; i += NT) dirty_g[i] = dirty[i];
-    if (tid == 0) st.pmax[b] = pm;
+            if ((inmask >> s) & 1) pup[(kyr + R) * NB + slot_kx(t, s) + R] = P[s];
+    }
+    if (towner) pup[(tp.x + R) * NB + tp.y + R] = Pt;
+    if (a.n_order > 0 && !aborted) {
+        if (tid == 0) {
+            float m2 = red[32];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) m2 = fmaxf(m2, red[32 + i]);
+            cst(ra, PMX_OFF + hown, make_float2(m2, 0.f));
+        }
+        if (handoff() && hown == 0 && tid == 0) {
+            float m2 = 0.f;
+#pragma unroll
+            for (int p = 0; p < KS; ++p) m2 = fmaxf(m2, cld(ra, PMX_OFF + p).x);
+            st.pmax[b] = sqrtf(m2);
+        }
+    }
+    if (hown == 0) {
+        for (int k = tid; k < a.nbt; k += NT) tmax_g[band_gtile(k)] = tmx[k];
+        for (int i = tid; i < nwords; i += NT) dirty_g[i] = dirty[i];
+    }
+    (void)pmx_part;
+    (void)pm;
 }
 
 // ------------------------------------------------------------------ host side
