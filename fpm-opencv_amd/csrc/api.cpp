@@ -390,7 +390,16 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &c->y0_dev, (size_t)prob->n_stack))) return fail(rc);
     if (c->path == FPM_PATH_GENERAL) {
         if (reg1024) c->meas_g = np;
-        if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
+        // fp16 spectrum storage on the Np 1024 register kernels: the row /
+        // column scratch T block-scaled in fp16 too (half its HBM traffic;
+        // FPM_T32=1 keeps it fp32)
+        if (reg1024 && fp16 && !getenv("FPM_T32")) {
+            if ((rc = dalloc(c, &st.T16, (size_t)B * nb * np))) return fail(rc);
+            if ((rc = dalloc(c, &st.tsr, (size_t)B * nb))) return fail(rc);
+            if ((rc = dalloc(c, &st.tsc, (size_t)B * np))) return fail(rc);
+        } else {
+            if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
+        }
         if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
         // patch groups on concurrent streams (FPM_PATCH_GROUPS=n overrides):

@@ -69,27 +69,6 @@ struct FzCfg {
     static constexpr int XT = XTILE;              // exchange tile per group (complex)
 };
 
-// store the column part h of a row IDFT (r[m] = x[t + 16 m]) into the part's
-// T row: row[16 m'] = r[h MPP + m'] (h is block-uniform; one unrolled branch
-// per part keeps every register index static)
-// pruned forward row DFT of column part h (input row[16 m'] = x[t + 16 (h MPP + m')])
-template <int NPARTS, class TW, int HH = 0>
-__device__ __forceinline__ void row_dft_part(const float2 *row, float2 (&v)[16], float2 (&o)[6], float2 *scr,
-                                             const TW &wt, int t, int xrd, int h) {
-    constexpr int MPP = 16 / NPARTS;
-    if constexpr (HH < NPARTS) {
-        if (HH == h) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
-#pragma unroll
-            for (int m = 0; m < MPP; ++m) v[HH * MPP + m] = row[16 * m];
-            dft256_inpart_out6<NPARTS, HH>(v, o, scr, wt, t, xrd);
-        } else {
-            row_dft_part<NPARTS, TW, HH + 1>(row, v, o, scr, wt, t, xrd, h);
-        }
-    }
-}
-
 // KS workgroups per patch: 1 (both column halves in turn), or split mode with
 // 2 / 4 workgroups each owning one column part
 template <int NT, int KS>
@@ -611,25 +590,27 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
         if (it > 0) pm = pm_of_red();  // the previous LED's pupil (:415)
-        // Straight-line over all slots: outside the support O = P = 0, so the
-        // numerator is exactly 0 and only the spectrum store and the tile
-        // bookkeeping need the mask.
+        // Only support pixels are updated: outside the support O = P = 0 and the
+        // numerator is exactly 0.  The mask is per lane, so a slot whose row
+        // misses the disk in every lane of the wave is skipped whole (exec
+        // zero): at r 33 the outer slots |kx| >= 32 of all rows |ky| > 8 and
+        // |kx| >= 16 of the rows |ky| > 28, 27 of the 96 (wave, row, slot)
+        // updates per LED.
 #pragma unroll
         for (int j = 0; j < RPG; ++j)
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                const int kx = slot_kx(t, s);
-                float2 num;
-                float oa;
-                const float2 nv = slot_update(F[j][s], Opre[j][s], P[j][s], pm, st, num, oa);
+                float2 num = make_float2(0.f, 0.f);
+                if ((inmask[j] >> s) & 1) {
+                    float oa;
+                    const float2 nv = slot_update(F[j][s], Opre[j][s], P[j][s], pm, st, num, oa);
+                    sst(srow + (kyr[j] * L + t) + soff(s), nv);  // read by a split partner
+                    note(yc + kyr[j], xc + slot_kx(t, s), oa, cmag(nv));
+                }
                 // park the numerator in this group's own exchange tile (idle
                 // until the next LED's pass A; 6 RPG 16 <= its 8 XP complex);
                 // a T row is too narrow for it when the part is 64 columns
                 scr[(j * 6 + s) * 16 + t] = num;
-                if ((inmask[j] >> s) & 1) {
-                    sst(srow + (kyr[j] * L + t) + soff(s), nv);  // read by a split partner
-                    note(yc + kyr[j], xc + kx, oa, cmag(nv));
-                }
             }
         if (towner) {
             // D = Objfup - ObjfcropP with ObjfcropP = tailX (gathered O*P): pass F = tailF

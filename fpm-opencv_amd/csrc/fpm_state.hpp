@@ -49,6 +49,12 @@ struct DevState {
     float2 *pupil;
     const uint16_t *meas;
     float2 *T;        // [B][nb][Np] row-transform scratch (general path)
+    // Np 1024 with fp16 spectrum storage (config 5): T held as __half2
+    // [B][nb][Np] (T == nullptr then), block-scaled by powers of two: the
+    // row IDFT stores each box row with its own scale (tsr, the inverse,
+    // [B][nb]), the column pass each column with its own (tsc, [B][Np])
+    __half2 *T16;
+    float *tsr, *tsc;
     float2 *dP;       // [B][nb][nb] pupil-update numerator (general path)
     float *tmax;      // [B][nty][ntx]
     unsigned *tdirty; // [B][ceil(ntx*nty/32)] fused path: tiles whose max is an upper bound
@@ -87,6 +93,9 @@ inline DevState patch_view(const DevState &st, int b0, int n) {
     if (v.pupil) v.pupil += b0 * nb2;
     if (v.meas) v.meas += (size_t)b0 * st.np * st.np;
     if (v.T) v.T += (size_t)b0 * st.nb * st.np;
+    if (v.T16) v.T16 += (size_t)b0 * st.nb * st.np;
+    if (v.tsr) v.tsr += (size_t)b0 * st.nb;
+    if (v.tsc) v.tsc += (size_t)b0 * st.np;
     if (v.dP) v.dP += b0 * nb2;
     if (v.tmax) v.tmax += (size_t)b0 * st.nty * st.ntx;
     if (v.tdirty) v.tdirty += (size_t)b0 * ((st.ntx * st.nty + 31) / 32);
@@ -111,6 +120,16 @@ __device__ __forceinline__ void spec_st(const DevState &st, int b, size_t i, flo
         st.spec16[o] = __float22half2_rn(make_float2(v.x * st.hscale, v.y * st.hscale));
     else
         st.spec[o] = v;
+}
+
+// block scale of fp16 scratch: a power of two s with m s < 2^14 for the
+// block's largest component magnitude m (m = 0: s = 1); returns s, *inv = 1/s
+__device__ __forceinline__ float h16_scale(float m, float *inv) {
+    int e = 0;
+    (void)frexpf(m, &e);  // m < 2^e
+    if (!(m > 0.f)) e = 0;
+    *inv = ldexpf(1.0f, e - 14);
+    return ldexpf(1.0f, 14 - e);
 }
 
 // ePIE update coefficient 1 / ((a + i c) m) of the general path for the

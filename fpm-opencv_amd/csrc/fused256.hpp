@@ -95,23 +95,52 @@ __device__ __forceinline__ void pdft16_inhalf(pf2 (&v)[16], pf2 (&r)[16]) {
     for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
 }
 
+// first radix-4 butterfly of a 16-point DFT with one non-zero input a in
+// position Q of (k1, k1+4, k1+8, k1+12): a -> (a, W4^Q a, W4^2Q a, W4^3Q a)
+template <bool INV, int Q>
+__device__ __forceinline__ void pbf4_one(pf2 a, pf2 &y0, pf2 &y1, pf2 &y2, pf2 &y3) {
+    const pf2 z = {0.f, 0.f};
+    if constexpr (Q == 0) {
+        y0 = a; y1 = a; y2 = a; y3 = a;
+    } else if constexpr (Q == 1) {   // pbf4 of (0, a, 0, 0)
+        y0 = a; y1 = padd_w4<INV>(z, a); y2 = -a; y3 = psub_w4<INV>(z, a);
+    } else if constexpr (Q == 2) {   // (0, 0, a, 0)
+        y0 = a; y1 = -a; y2 = a; y3 = -a;
+    } else {                         // (0, 0, 0, a)
+        y0 = a; y1 = psub_w4<INV>(z, a); y2 = -a; y3 = padd_w4<INV>(z, a);
+    }
+}
+
 // 16-point DFT whose input is zero outside v[4Q .. 4Q+3] (one quarter of a
 // row, split mode with four workgroups per patch): the first radix-4 stage
-// sees one non-zero input per butterfly, a -> (a, W4^Q a, W4^2Q a, W4^3Q a)
+// sees one non-zero input per butterfly
 template <bool INV, int Q>
 __device__ __forceinline__ void pdft16_inquarter(pf2 (&v)[16], pf2 (&r)[16]) {
-    const pf2 z = {0.f, 0.f};
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1) {
         const pf2 a = v[k1 + 4 * Q];
-        if constexpr (Q == 0) {
-            v[k1] = a; v[k1 + 4] = a; v[k1 + 8] = a; v[k1 + 12] = a;
-        } else if constexpr (Q == 1) {   // pbf4 of (0, a, 0, 0)
-            v[k1] = a; v[k1 + 4] = padd_w4<INV>(z, a); v[k1 + 8] = -a; v[k1 + 12] = psub_w4<INV>(z, a);
-        } else if constexpr (Q == 2) {   // (0, 0, a, 0)
-            v[k1] = a; v[k1 + 4] = -a; v[k1 + 8] = a; v[k1 + 12] = -a;
-        } else {                         // (0, 0, 0, a)
-            v[k1] = a; v[k1 + 4] = psub_w4<INV>(z, a); v[k1 + 8] = -a; v[k1 + 12] = padd_w4<INV>(z, a);
+        pbf4_one<INV, Q>(a, v[k1], v[k1 + 4], v[k1 + 8], v[k1 + 12]);
+    }
+    pmid_tw<INV>(v);
+    pstage2<INV>(v);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
+}
+
+// 16-point DFT whose input is zero outside v[2E], v[2E + 1] (one eighth of a
+// row, distributed mode with eight workgroups per patch): two of the first
+// stage's butterflies see one non-zero input, the other two none
+template <bool INV, int E>
+__device__ __forceinline__ void pdft16_ineighth(pf2 (&v)[16], pf2 (&r)[16]) {
+    constexpr int Q = E >> 1, K0 = (2 * E) & 3;
+    const pf2 z = {0.f, 0.f};
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        if (k1 == K0 || k1 == K0 + 1) {
+            const pf2 a = v[k1 + 4 * Q];
+            pbf4_one<INV, Q>(a, v[k1], v[k1 + 4], v[k1 + 8], v[k1 + 12]);
+        } else {
+            v[k1] = z; v[k1 + 4] = z; v[k1 + 8] = z; v[k1 + 12] = z;
         }
     }
     pmid_tw<INV>(v);
@@ -190,10 +219,11 @@ __device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[
     if constexpr (NPARTS == 2) {
         dft256_inhalf_out6<P>(v, o, scr, wt, t, xrd);
     } else {
-        static_assert(NPARTS == 4, "two or four column parts");
+        static_assert(NPARTS == 4 || NPARTS == 8, "two, four or eight column parts");
         pf2 pv[16], py[16], po[6];
         to_pk(v, pv);
-        pdft16_inquarter<false, P>(pv, py);
+        if constexpr (NPARTS == 4) pdft16_inquarter<false, P>(pv, py);
+        else pdft16_ineighth<false, P>(pv, py);
         ptwiddle15<false>(py, wt);
         float2 y[16];
         from_pk(py, y);
@@ -201,6 +231,27 @@ __device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[
         to_pk(v, pv);
         pdft16_out6<false>(pv, po);
         from_pk(po, o);
+    }
+}
+
+// pruned forward row DFT of column part h (block-uniform, 0 <= h < NPARTS):
+// input row[16 m'] = x[t + 16 (h MPP + m')], m' < MPP = 16 / NPARTS, output
+// o[s] = the part's contribution to X[t + 16 SK[s]].  One unrolled branch per
+// part keeps every register index static.
+template <int NPARTS, class TW, int HH = 0>
+__device__ __forceinline__ void row_dft_part(const float2 *row, float2 (&v)[16], float2 (&o)[6], float2 *scr,
+                                             const TW &wt, int t, int xrd, int h) {
+    constexpr int MPP = 16 / NPARTS;
+    if constexpr (HH < NPARTS) {
+        if (HH == h) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int m = 0; m < MPP; ++m) v[HH * MPP + m] = row[16 * m];
+            dft256_inpart_out6<NPARTS, HH>(v, o, scr, wt, t, xrd);
+        } else {
+            row_dft_part<NPARTS, TW, HH + 1>(row, v, o, scr, wt, t, xrd, h);
+        }
     }
 }
 

@@ -61,7 +61,13 @@ constexpr int XT = 10 * XP;               // exchange tile per group (complex)
 // land on disjoint banks (106 * 2 dwords = 20 mod 64); with stride 100 they
 // overlapped two ways (the 16-byte row reads stay conflict-free either way).
 constexpr int kXtFast = 106;
-constexpr int TLD = NP + 1;               // T row pitch (complex)
+constexpr int TLD = NP + 1;               // T row pitch (complex), dense
+// T row pitch when LDS allows: 202 = 10 (mod 32), so the column reads of
+// pass B (consecutive rows for the ten lanes of a group, adjacent columns for
+// the groups) and the row accesses of passes A / C spread over the banks
+// (tools/lds_s90.py --mr: modelled LDS-array cycles of the T accesses 6056 ->
+// 4150 per LED, conflict-free 3096)
+constexpr int TLD_FAST = 202;
 }  // namespace fm
 
 struct FusedMRArgs {
@@ -74,6 +80,7 @@ struct FusedMRArgs {
     float rnbx;
     unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles, else null
     int xt;                    // exchange-tile stride per group (complex): kXtFast or fm::XT
+    int tld;                   // T row pitch (complex): TLD_FAST or fm::TLD
 };
 
 __device__ __forceinline__ int mr_slot_k(int s) { return fm::SK[s]; }
@@ -86,6 +93,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     const DevState &st = a.st;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *tiles = sm;                        // NG * XT exchange tiles
+    const int TLD = a.tld;
     float2 *th = tiles + NG * a.xt;            // (NB + 2) * TLD: T rows, zero row, dummy row
     float2 *tw2 = th + (NB + 2) * TLD;         // [m1][l] = W200^{l m1}
     float *red = (float *)(tw2 + 200);         // 48
@@ -272,17 +280,17 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
-        if (ron) {
+        if (ron) {  // support pixels only (a slot off the disk in the whole wave is skipped)
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                float2 num;
-                float oa;
-                const float2 nv = slot_update(F[s], Opre[s], P[s], pm, st, num, oa);
-                th[g * TLD + s * 10 + l] = num;
+                float2 num = make_float2(0.f, 0.f);
                 if ((inmask >> s) & 1) {
+                    float oa;
+                    const float2 nv = slot_update(F[s], Opre[s], P[s], pm, st, num, oa);
                     (srow + (kyr * L + l))[soff(s)] = nv;
                     note(yc + kyr, xc + mr_kx(l, s), oa, cmag(nv));
                 }
+                th[g * TLD + s * 10 + l] = num;
             }
         }
         FPM_STAMP(9)
@@ -388,8 +396,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 
 // ------------------------------------------------------------------ host side
 namespace {
-size_t mr_lds_bytes(int nb, int nbt, int xt = fm::XT) {
-    return (size_t)(fm::NG * xt + (nb + 2) * fm::TLD + 200) * sizeof(float2) + 48 * sizeof(float) +
+size_t mr_lds_bytes(int nb, int nbt, int xt = fm::XT, int tld = fm::TLD) {
+    return (size_t)(fm::NG * xt + (nb + 2) * tld + 200) * sizeof(float2) + 48 * sizeof(float) +
            64 * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) +
            sizeof(int);
 }
@@ -423,8 +431,12 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
     a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
     a.rnbx = 1.0f / (float)a.nbx;
     a.dbg = dbg;
-    a.xt = mr_lds_bytes(st.nb, a.nbt, fm::kXtFast) <= 160 * 1024 ? fm::kXtFast : fm::XT;
-    const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xt);
+    // bank-friendly strides while LDS allows: tiles first, then the T pitch
+    // (FPM_MR_DENSE=1 forces the dense layout, test_gpu_fused_mr.py)
+    const bool dense = getenv("FPM_MR_DENSE") != nullptr;
+    a.xt = !dense && mr_lds_bytes(st.nb, a.nbt, fm::kXtFast) <= 160 * 1024 ? fm::kXtFast : fm::XT;
+    a.tld = !dense && mr_lds_bytes(st.nb, a.nbt, a.xt, fm::TLD_FAST) <= 160 * 1024 ? fm::TLD_FAST : fm::TLD;
+    const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xt, a.tld);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_mr, dim3(st.B), dim3(fm::NT), lds, s, a);

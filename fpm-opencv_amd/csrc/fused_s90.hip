@@ -25,6 +25,8 @@
 // box row in registers (kx = fold(l + 10 k)).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "cpk.hpp"
 #include "dft90.hpp"
 #include "fft_lds.hpp"
@@ -40,8 +42,23 @@ constexpr int GPW = 6;                 // groups per wave (lanes 60..63 idle)
 constexpr int NT = 1024;               // 16 waves: 4 per SIMD (128-VGPR budget)
 constexpr int NW = NT / 64;
 constexpr int NG = NW * GPW;           // 96 groups >= 90 columns
+static_assert(NG >= NP, "one group per column");
 constexpr int XT = 10 * kXP90;         // exchange tile per group (complex)
-constexpr int TLD = NP + 1;            // T row pitch (complex)
+constexpr int TLD = NP + 1;            // T row pitch (complex), dense layout
+// LDS bank layout (tools/lds_s90.py models every LDS instruction of an LED
+// step with the gfx950 lane-group table).  Dense layout: tiles at a uniform
+// stride of 100 and T rows of pitch 91 put 45 % of the modelled LDS-array
+// cycles into bank conflicts (SQ counted 28 % at config 2): the 8-byte tile
+// row writes of the two groups sharing a 16-lane batch overlap, and so do
+// the column reads of T.  Conflict-light layout (when LDS allows, r <= 30):
+// the six tiles of a wave at offsets with residues 0, 26, 6, 4, 30, 26
+// (mod 32 complex), found by a search over the tile writes and the 16-byte
+// row reads, in a 704-complex wave slot (704 = 0 mod 32, so every wave sees
+// the same banks), and T rows of pitch 106 (= 10 mod 32).
+constexpr int XW_DENSE = GPW * XT;     // wave slot of the dense layout
+constexpr int XW_FAST = 704;
+constexpr int XG_FAST[GPW] = {0, 122, 230, 356, 478, 602};
+constexpr int TLD_FAST = 106;
 constexpr int RMAX = 44;               // 2 r + 1 <= Np
 }  // namespace f90
 
@@ -53,7 +70,9 @@ struct FusedS90Args {
     int n_order;
     int btx0, bty0, nbx, nbt;  // live-band tiles (fpm_fused.hip FusedArgs)
     float rnbx;
-    int xt;                    // exchange-tile stride per group (complex)
+    int xw;                    // exchange tiles: wave slot (complex)
+    int xg[f90::GPW];          // tile offset of group gw in the wave slot
+    int tld;                   // T row pitch (complex)
     unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles (fused_mr.hip's slots), else null
 };
 
@@ -66,7 +85,8 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     const DevState &st = a.st;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *tiles = sm;                        // NG * xt exchange tiles
-    float2 *th = tiles + NG * a.xt;            // (NB + 2) * TLD: T rows, zero row, dummy row
+    const int TLD = a.tld;
+    float2 *th = tiles + NW * a.xw;            // (NB + 2) * TLD: T rows, zero row, dummy row
     float2 *tw = th + (NB + 2) * TLD;          // [a][b] = W90^{a b}, a, b < 10
     float *red = (float *)(tw + 100);          // 48
     int *rowoff = (int *)(red + 48);           // 90: T offset of FFT row y (the zero row outside the box)
@@ -79,7 +99,10 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     const int l = act ? lane - N2 * gw : 0;    // lane within the group
     const int g = w * GPW + (act ? gw : 0);    // group in the workgroup
     const int b = blockIdx.x;
-    float2 *tile = tiles + g * a.xt;
+    int xgo = a.xg[0];  // group offset (uniform kernel-argument values, selected per lane)
+#pragma unroll
+    for (int i = 1; i < GPW; ++i) xgo = gw == i ? a.xg[i] : xgo;
+    float2 *tile = tiles + w * a.xw + xgo;
     const int xrd = opaque_i(l * kXP90);
     const int nwords = (a.nbt + 31) >> 5;
 
@@ -351,8 +374,8 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
 
 // ------------------------------------------------------------------ host side
 namespace {
-size_t s90_lds_bytes(int nb, int nbt, int xt) {
-    return (size_t)(f90::NG * xt + (nb + 2) * f90::TLD + 100) * sizeof(float2) + 48 * sizeof(float) +
+size_t s90_lds_bytes(int nb, int nbt, int xw, int tld) {
+    return (size_t)(f90::NW * xw + (nb + 2) * tld + 100) * sizeof(float2) + 48 * sizeof(float) +
            f90::NP * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
 }
 }  // namespace
@@ -364,7 +387,7 @@ bool fused_s90_supported(int np, int r, const DevState &st) {
         return false;
     const int bty0 = st.sy0 / kTile, btx0 = st.sx0 / kTile;
     const int nbx = st.sx1 / kTile - btx0 + 1, nbt = nbx * (st.sy1 / kTile - bty0 + 1);
-    return s90_lds_bytes(2 * r + 1, nbt, f90::XT) <= 160 * 1024;
+    return s90_lds_bytes(2 * r + 1, nbt, f90::XW_DENSE, f90::TLD) <= 160 * 1024;
 }
 
 hipError_t launch_fused_s90_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
@@ -384,9 +407,13 @@ hipError_t launch_fused_s90_iteration(const DevState &st, const uint16_t *meas, 
     a.nbx = st.sx1 / kTile - a.btx0 + 1;
     a.nbt = a.nbx * (st.sy1 / kTile - a.bty0 + 1);
     a.rnbx = 1.0f / (float)a.nbx;
-    a.xt = f90::XT;
+    // the conflict-light layout when it fits (FPM_S90_DENSE=1 forces the dense one)
+    const bool fast = !getenv("FPM_S90_DENSE") && s90_lds_bytes(st.nb, a.nbt, f90::XW_FAST, f90::TLD_FAST) <= 160 * 1024;
+    a.xw = fast ? f90::XW_FAST : f90::XW_DENSE;
+    for (int i = 0; i < f90::GPW; ++i) a.xg[i] = fast ? f90::XG_FAST[i] : i * f90::XT;
+    a.tld = fast ? f90::TLD_FAST : f90::TLD;
     a.dbg = dbg;
-    const size_t lds = s90_lds_bytes(st.nb, a.nbt, a.xt);
+    const size_t lds = s90_lds_bytes(st.nb, a.nbt, a.xw, a.tld);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_s90, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_s90, dim3(st.B), dim3(f90::NT), lds, s, a);

@@ -203,6 +203,21 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     pmx = wave_max(pmx);
     if (lane == 0) st.pmax[(size_t)b * st.npart + row] = pmx;
     w1k_DN<true>(x, wt, twL, c, t, xrd);                                 // :365 (rows)
+    if (st.T16) {  // fp16 scratch: one power-of-two scale per box row
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m = fmaxf(m, fmaxf(fabsf(x[j].x), fabsf(x[j].y)));
+        float inv;
+        const float sc = h16_scale(wave_max(m), &inv);
+        __half2 *T = st.T16 + ((size_t)b * nb + row) * N + t + 64 * c;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+                T[16 * bb + 256 * p] = __float22half2_rn(make_float2(x[4 * p + bb].x * sc, x[4 * p + bb].y * sc));
+        if (lane == 0) st.tsr[(size_t)b * nb + row] = inv;
+        return;
+    }
     float2 *T = st.T + ((size_t)b * nb + row) * N + t + 64 * c;
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -226,12 +241,19 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
     constexpr int G = N / CW;
     const int cg = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);
     const int r = st.r, nb = st.nb, b = blockIdx.y, x0 = cg * CW;
-    float2 *T = st.T + (size_t)b * nb * N + x0;
+    float2 *T = st.T ? st.T + (size_t)b * nb * N + x0 : nullptr;
+    __half2 *T16 = st.T16 ? st.T16 + (size_t)b * nb * N + x0 : nullptr;
     // FFT row i of a column is box row j = i + r (i <= r) or i - N + r
     // (i >= N - r) (:364: every other row is zero)
     for (int idx = threadIdx.x; idx < nb * CW; idx += NTC) {
         const int j = idx / CW, cc = idx - j * CW;
-        strip[j * SPCC + cc] = T[(size_t)j * N + cc];
+        if (T16) {
+            const float2 h = __half22float2(T16[(size_t)j * N + cc]);
+            const float is = st.tsr[(size_t)b * nb + j];
+            strip[j * SPCC + cc] = make_float2(h.x * is, h.y * is);
+        } else {
+            strip[j * SPCC + cc] = T[(size_t)j * N + cc];
+        }
     }
     __syncthreads();
     auto boxrow = [&](int i) { return i <= r ? i + r : (i >= N - r ? i - N + r : -1); };
@@ -259,18 +281,28 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
         x[j] = make_float2(v.x * s, v.y * s);
     }
     w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (columns)
+    float sc = 1.f;
+    if (T16) {  // fp16 scratch: one power-of-two scale per column (over all its rows)
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m = fmaxf(m, fmaxf(fabsf(x[j].x), fabsf(x[j].y)));
+        float inv;
+        sc = h16_scale(wave_max(m), &inv);
+        if ((threadIdx.x & 63) == 0) st.tsc[(size_t)b * N + x0 + w] = inv;
+    }
     __syncthreads();  // every wave is done with its tile before the strip is rewritten
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int j = boxrow(t + 16 * (4 * c + bb) + 256 * p);
-            if (j >= 0) strip[j * SPCC + w] = x[4 * p + bb];
+            if (j >= 0) strip[j * SPCC + w] = make_float2(x[4 * p + bb].x * sc, x[4 * p + bb].y * sc);
         }
     __syncthreads();
     for (int idx = threadIdx.x; idx < nb * CW; idx += NTC) {
         const int j = idx / CW, cc = idx - j * CW;
-        T[(size_t)j * N + cc] = strip[j * SPCC + cc];
+        if (T16) T16[(size_t)j * N + cc] = __float22half2_rn(strip[j * SPCC + cc]);
+        else T[(size_t)j * N + cc] = strip[j * SPCC + cc];
     }
 }
 
@@ -289,10 +321,21 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     pm = block_max(pm, red);
     if (row >= nb) return;
     const int ky = row - r, w2 = r * r - ky * ky;
-    const float2 *Tr = st.T + ((size_t)b * nb + row) * N + c;
     float2 x[16];
+    if (st.T16) {  // column j's element times its column scale
+        const __half2 *Tr = st.T16 + ((size_t)b * nb + row) * N + c;
+        const float *is = st.tsc + (size_t)b * N + c;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = Tr[4 * (t + 16 * j)];
+        for (int j = 0; j < 16; ++j) {
+            const float2 h = __half22float2(Tr[4 * (t + 16 * j)]);
+            const float s = is[4 * (t + 16 * j)];
+            x[j] = make_float2(h.x * s, h.y * s);
+        }
+    } else {
+        const float2 *Tr = st.T + ((size_t)b * nb + row) * N + c;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = Tr[4 * (t + 16 * j)];
+    }
     w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (rows)
     float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
     float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;

@@ -98,3 +98,24 @@ def test_np200_more_patches_than_cus():
         ref = oracle_lib.run_fpm(stack[:, b], order, x0, y0, Np, L, r, 10, 3, 1)
         assert rel_l2(out["objCrop"][b], ref["objCrop"]) < 1e-5, b
         assert rel_l2(out["pupil"][b], ref["pupil"]) < 1e-5, b
+
+
+def test_np200_lds_layouts_bit_identical():
+    """Bank-friendly strides (exchange-tile stride 106, T pitch 202, whatever
+    LDS allows) and the dense layout (FPM_MR_DENSE=1) move the same values
+    through different LDS addresses: bit-identical results."""
+    import os
+    r, iters = 26, 2
+    x0, y0, order = grid_geometry(Np, L, 4, 20)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=67)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 10, 3, n_patch=2, path=fpm_amd.PATH_FUSED)
+    outs = []
+    for dense in (False, True):
+        if dense:
+            os.environ["FPM_MR_DENSE"] = "1"
+        try:
+            outs.append(fpm_amd.run_fpm(prob, stack, iters))
+        finally:
+            os.environ.pop("FPM_MR_DENSE", None)
+    for k in ("objF", "objCrop", "pupil"):
+        np.testing.assert_array_equal(outs[0][k], outs[1][k])

@@ -84,3 +84,21 @@ def test_s90_deterministic_and_iterations_compose():
             outs.append(s.download())
     for k in ("objF", "objCrop", "pupil"):
         np.testing.assert_array_equal(outs[0][k], outs[1][k])
+
+
+def test_s90_lds_layouts_bit_identical():
+    """The conflict-light LDS layout (r <= 30: shifted exchange tiles, T pitch
+    106) and the dense one (FPM_S90_DENSE=1, also what r > 30 runs) move the
+    same values through different LDS addresses: results are bit-identical."""
+    Np, L, r = 90, 360, 30
+    x0, y0, order = grid_geometry(Np, L, 4, 22)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=95)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2, path=fpm_amd.PATH_FUSED)
+    fast = _solve(prob, stack, 2)
+    os.environ["FPM_S90_DENSE"] = "1"
+    try:
+        dense = _solve(prob, stack, 2)
+    finally:
+        os.environ.pop("FPM_S90_DENSE", None)
+    for k in ("objF", "objCrop", "pupil"):
+        np.testing.assert_array_equal(fast[k], dense[k])

@@ -71,3 +71,25 @@ def test_np1024_stack_layout_round_trip():
     with fpm_amd.Solver(fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2)) as s:
         s.upload(stack)
         np.testing.assert_array_equal(s.download_stack(), stack)
+
+
+def test_np1024_fp16_scratch_vs_fp32_scratch():
+    """fp16 spectrum storage puts the Np 1024 row / column scratch T in
+    block-scaled fp16 too (one power-of-two scale per box row after the row
+    IDFT, per column after the column pass); FPM_T32=1 keeps it fp32.  The two
+    differ by fp16 rounding of T (2^-11 relative per element), well inside
+    config 5's 1e-2."""
+    L, r = 2048, 333
+    x0, y0, order = grid_geometry(Np, L, 2, 100)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=87)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2, flags=fpm_amd.FLAG_SPEC_FP16)
+    h = _run(prob, stack, 2)
+    os.environ["FPM_T32"] = "1"
+    try:
+        f = _run(prob, stack, 2)
+    finally:
+        os.environ.pop("FPM_T32", None)
+    for k in ("objF", "objCrop", "pupil"):
+        for b in range(2):
+            e = rel_l2(h[k][b], f[k][b])
+            assert 0 < e < 2e-3, (k, b, e)

@@ -30,13 +30,16 @@ def lanes():
     return out
 
 
-def sites(xt, xp, tld, w=1):
+DENSE = (600, [100 * g for g in range(6)], 91)
+FAST = (704, [0, 122, 230, 356, 478, 602], 106)  # fused_s90.hip XW_FAST / XG_FAST / TLD_FAST
+
+
+def sites(xw, xg, tld, w=1, xp=10):
     """(kind, byte addresses, repeat) of the wave's LDS instructions per LED.
-    xt: exchange-tile stride per group (complex), xp: exchange row pitch
-    (complex), tld: T row pitch (complex).  Wave w (groups 6w..6w+5)."""
+    xw: wave slot of the exchange tiles, xg: tile offset of each group in it,
+    xp: exchange row pitch, tld: T row pitch (all complex).  Wave w."""
     L = lanes()
-    tiles = 0
-    th = NW * GPW * xt  # T after the tiles (complex)
+    th = NW * xw  # T after the tiles (complex)
     rowoff = [(fold(y) + R) * tld if -R <= fold(y) <= R else NB * tld for y in range(NP)]
     out = []
 
@@ -46,14 +49,17 @@ def sites(xt, xp, tld, w=1):
     def gidx(gw):
         return w * GPW + gw
 
+    def tb(gw):
+        return w * xw + xg[gw]
+
     # exchange: write rows m (9 or 10), read lane's row l
     for nrows, nread in ((9, 5), (10, 4)):  # ab: 9 rows written, 10 read (5 x b128); ba: 10 written, 9 read
         for m in range(nrows):
-            out.append(("write_b64", addr(lambda gw, l: tiles + gidx(gw) * xt + m * xp + l), 1))
+            out.append(("write_b64", addr(lambda gw, l: tb(gw) + m * xp + l), 1))
         for i in range(nread):
-            out.append(("read_b128", addr(lambda gw, l: tiles + gidx(gw) * xt + l * xp + 2 * i), 1))
+            out.append(("read_b128", addr(lambda gw, l: tb(gw) + l * xp + 2 * i), 1))
         if nread == 4:
-            out.append(("read_b64", addr(lambda gw, l: tiles + gidx(gw) * xt + l * xp + 8), 1))
+            out.append(("read_b64", addr(lambda gw, l: tb(gw) + l * xp + 8), 1))
     # each LED runs ab twice (A, B) and ba twice (B, C)
     ex = [(k, a, 2) for k, a, _ in out]
     # T: A writes row g: th[g tld + l + 9 m], l < 9
@@ -73,34 +79,18 @@ def sites(xt, xp, tld, w=1):
     return ex, tl
 
 
-def report(xt, xp, tld):
-    res = []
+def report(xw, xg, tld):
+    ce = ie = ct = it = 0
     for w in range(NW):
-        ex, tl = sites(xt, xp, tld, w)
-        res.append((total(ex), total(tl)))
-    ce = sum(r[0][0] for r in res)
-    ie = sum(r[0][1] for r in res)
-    ct = sum(r[1][0] for r in res)
-    it = sum(r[1][1] for r in res)
+        ex, tl = sites(xw, xg, tld, w)
+        a, b, _ = total(ex)
+        c, d, _ = total(tl)
+        ce, ie, ct, it = ce + a, ie + b, ct + c, it + d
     return ce, ie, ct, it
 
 
 if __name__ == "__main__":
-    ce, ie, ct, it = report(100, 10, 91)
-    print(f"current xt 100 xp 10 tld 91: exchange {ce} cyc (ideal {ie}, {1 - ie / ce:.2f} conflict), "
-          f"T {ct} (ideal {it}, {1 - it / ct:.2f}); total share {(ce + ct - ie - it) / (ce + ct):.2f}")
-    best = []
-    for xp in (10, 11, 12):
-        for xt in range(10 * xp, 10 * xp + 40, 2):
-            ce, ie, ct, it = report(xt, xp, 91)
-            best.append((ce, xt, xp, ie))
-    best.sort()
-    for ce, xt, xp, ie in best[:8]:
-        print(f"exchange xt {xt} xp {xp}: {ce} cyc (ideal {ie})")
-    bt = []
-    for tld in range(91, 110):
-        ce, ie, ct, it = report(100, 10, tld)
-        bt.append((ct, tld, it))
-    bt.sort()
-    for ct, tld, it in bt[:6]:
-        print(f"T tld {tld}: {ct} cyc (ideal {it})")
+    for name, lay in (("dense", DENSE), ("fast", FAST)):
+        ce, ie, ct, it = report(*lay)
+        print(f"{name} {lay}: exchange {ce} LDS cycles (conflict-free {ie}), T {ct} ({it}); "
+              f"conflict share {(ce + ct - ie - it) / (ce + ct):.2f}")
