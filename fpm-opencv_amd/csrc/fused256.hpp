@@ -127,28 +127,6 @@ __device__ __forceinline__ void pdft16_inquarter(pf2 (&v)[16], pf2 (&r)[16]) {
     for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
 }
 
-// 16-point DFT whose input is zero outside v[2E], v[2E + 1] (one eighth of a
-// row, distributed mode with eight workgroups per patch): two of the first
-// stage's butterflies see one non-zero input, the other two none
-template <bool INV, int E>
-__device__ __forceinline__ void pdft16_ineighth(pf2 (&v)[16], pf2 (&r)[16]) {
-    constexpr int Q = E >> 1, K0 = (2 * E) & 3;
-    const pf2 z = {0.f, 0.f};
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) {
-        if (k1 == K0 || k1 == K0 + 1) {
-            const pf2 a = v[k1 + 4 * Q];
-            pbf4_one<INV, Q>(a, v[k1], v[k1 + 4], v[k1 + 8], v[k1 + 12]);
-        } else {
-            v[k1] = z; v[k1 + 4] = z; v[k1 + 8] = z; v[k1 + 12] = z;
-        }
-    }
-    pmid_tw<INV>(v);
-    pstage2<INV>(v);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) r[m] = v[4 * (m & 3) + (m >> 2)];
-}
-
 // Four-step twiddles W256^{m t} (m = 0..15) of lane t, held in 32 VGPRs for a
 // whole pass: a table read per use serialised on LDS latency at two waves per
 // SIMD.
@@ -219,11 +197,10 @@ __device__ __forceinline__ void dft256_inpart_out6(float2 (&v)[16], float2 (&o)[
     if constexpr (NPARTS == 2) {
         dft256_inhalf_out6<P>(v, o, scr, wt, t, xrd);
     } else {
-        static_assert(NPARTS == 4 || NPARTS == 8, "two, four or eight column parts");
+        static_assert(NPARTS == 4, "two or four column parts");
         pf2 pv[16], py[16], po[6];
         to_pk(v, pv);
-        if constexpr (NPARTS == 4) pdft16_inquarter<false, P>(pv, py);
-        else pdft16_ineighth<false, P>(pv, py);
+        pdft16_inquarter<false, P>(pv, py);
         ptwiddle15<false>(py, wt);
         float2 y[16];
         from_pk(py, y);

@@ -18,12 +18,10 @@
 //   sync 1   (also carries each part's max|P| partial of the previous LED)
 //   B        Tg[box rows][own columns] -> LDS, column IDFT, 1/Np^2,
 //            amplitude replacement, column DFT (pass B of fpm_fused.hip
-//            verbatim), box rows stay in LDS                           (:365-394)
-//   C        row-DFT partials over the own columns of EVERY row, straight
-//            from LDS (all 32 groups busy, as split mode's pass C), pruned
-//            to the support columns -> published for the row owners      (:394)
+//            verbatim), box rows back to Tg                              (:365-394)
 //   sync 2
-//   F        the owner of a row sums the KS partials in part order
+//   C        row DFTs of the own rows from Tg (full input), pruned to the
+//            support columns -> F complete, no partial sums               (:394)
 //   update   object update of the own rows on the support (:405-447), pupil
 //            numerator (:457-464), tile maxima of |spec| in LDS
 //   sync 3   (carries the window's tile maxima / dirty bits)
@@ -32,18 +30,12 @@
 //   max      exact max|objF| (:460,467), redundant in every part (identical)
 //   P        P += num / max|objF| on the own rows (:468-475), max|P| partial
 //
-// Handoffs: one monotone flag per part (3 per LED); Tg, the row-DFT
-// partials, the tile publications and the spectrum move with device-coherent
-// policies (plain
+// Handoffs: one monotone flag per part (3 per LED); Tg, the tile
+// publications and the spectrum move with device-coherent policies (plain
 // stores + L1-bypassing loads when every part of the patch sits on one XCD --
 // the L2 is the coherence point -- sc1 otherwise), see fused_sync.hpp.
-// Tg needs no double buffering: in A a part writes only its own rows, in B
-// it reads only its own columns, and every phase change is behind a handoff.
-// Neither do the partials: a part writes those of LED it + 1 after sync 1 of
-// LED it + 1, which every owner publishes after it has summed the LED-it ones.
-// (Round 3's pass C read the own rows' full T from Tg after B had written its
-// columns back: one more T round trip through the L2, and only 64/KS of the
-// 32 groups busy in the row DFTs.)
+// Tg needs no double buffering: in A and C a part touches only its own rows,
+// in B only its own columns, and every phase change is behind a handoff.
 #include <hip/hip_runtime.h>
 
 #include "dft16.hpp"
@@ -58,12 +50,9 @@ namespace fpm {
 namespace {
 constexpr int kTgRows = fz::NROWS + fz::MAXTAILROWS;  // Tg rows: 64 FFT rows + tail rows
 constexpr int kWinTiles = 64;                         // window tiles published per part (<= 6 x 6 used)
-constexpr int kPartElems = fz::NROWS * 96 + fz::MAXTAIL;  // one part's row-DFT partials: [row][slot][t], tail pixels
 // per-patch distributed-mode area (float2): Tg, then KS x kWinTiles tile
-// publications (max, dirty flag), KS max|P| partials, KS x kPartElems partials
-constexpr size_t dist_patch_elems(int ks) {
-    return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + ks + (size_t)ks * kPartElems;
-}
+// publications (max, dirty flag), then KS max|P| partials
+constexpr size_t dist_patch_elems(int ks) { return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + ks; }
 }  // namespace
 
 template <int KS>
@@ -82,7 +71,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     float2 *tw2 = th + (nrows + 2) * TLD;           // [m][t] = W256^{m t}
     float2 *tw = tw2 + 256;                         // W256^k
     float2 *tailX = tw + 256;                       // MAXTAIL
-    float *red = (float *)(tailX + MAXTAIL);        // 48: clean / dirty / pupil maxima per wave
+    float2 *tailF = tailX + MAXTAIL;                // MAXTAIL
+    float *red = (float *)(tailF + MAXTAIL);        // 48: clean / dirty / pupil maxima per wave
     int *sig = (int *)(red + 48);                   // 96: T row of ky in [-48, 47], -1 outside the box
     int2 *tpx = (int2 *)(sig + 96);                 // MAXTAIL tail pixels (ky, kx)
     int *tpq = (int *)(tpx + MAXTAIL);              // MAXTAIL: tail row of each tail pixel
@@ -105,7 +95,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * XTILE;
     const int nwords = (a.nbt + 31) >> 5;
-    constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles, PART_OFF = PMX_OFF + KS;
+    constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
 
     // ---- one-time setup
     if (tid == 0) {
@@ -390,44 +380,15 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 }
             }
         }
-        __syncthreads();  // own columns of T (box rows) complete in LDS
-
-        // ---- C: row-DFT partials over the own columns, every row (:394)
-        {
-            const int pbase = PART_OFF + hown * kPartElems;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int i = g + NG * j;  // FFT row
-                if (i >= a.n_fft_rows) continue;  // group-uniform
-                float2 o[6];
-                row_dft_part<KS>(th + i * TLD + t, v, o, scr, wt, t, xrd, hown);
-                const int ky = a.ky_lo + i;
-#pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    const int kx = slot_kx(t, s);
-                    if (ky * ky + kx * kx <= R * R) cst(ra, pbase + (i * 6 + s) * 16 + t, o[s]);  // the owner's support
-                }
-            }
-            // tail pixels: 16 lanes sum the part's TH columns of the pixel's row
-            for (int pp = g; pp < a.n_tail_px; pp += NG) {
-                const int2 px = tpx[pp];
-                const float2 *row = th + sig[px.x + KYOFF] * TLD;
-                pf2 s2p = {0.f, 0.f};
-                pf2 wk = pin(tw[((t + TH * hown) * (px.y + NP)) & (NP - 1)]);
-                const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
-#pragma unroll
-                for (int m = 0; m < TH / 16; ++m) {
-                    s2p += pmul(pin(row[t + 16 * m]), wk);
-                    if (m < TH / 16 - 1) wk = pmul(wk, wstep);
-                }
-                float2 s2 = pout(s2p);
-#pragma unroll
-                for (int o = 8; o > 0; o >>= 1) {
-                    s2.x += __shfl_xor(s2.x, o, 64);
-                    s2.y += __shfl_xor(s2.y, o, 64);
-                }
-                if (t == 0) cst(ra, pbase + NROWS * 96 + pp, s2);
-            }
+        __syncthreads();
+        for (int i = tid; i < nrows * (TH / 2); i += NT) {  // 16-byte stores
+            const int row = i / (TH / 2), c2 = i - row * (TH / 2);
+            const float2 e0 = th[row * TLD + 2 * c2], e1 = th[row * TLD + 2 * c2 + 1];
+            typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+            const u32x4_t d = {__float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e1.x), __float_as_uint(e1.y)};
+            const int off = (row * NP + TH * hown + 2 * c2) * (int)sizeof(float2);
+            if (local) __builtin_amdgcn_raw_buffer_store_b128(d, ra, off, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b128(d, ra, off, 0, 16);
         }
         FPM_STAMP(3)
         if (!handoff()) {  // ---- sync 2
@@ -436,42 +397,38 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         FPM_STAMP(4)
 
-        // ---- F of the own rows: the KS partials summed in part order (the
-        // same order for every row, so the result does not depend on which
-        // part owns it), spread over all threads: element e = (k, s, t') of
-        // own row k, slot s, lane t' -> the owning group's exchange tile
-        // (free until the update parks its numerators there, slot for slot)
-        {
-            constexpr int NE = NOWN * 96, PER = (NE + NT - 1) / NT;
-#pragma unroll 1
-            for (int q = 0; q < PER; ++q) {
-                const int e = tid + NT * q;
-                const int k = e / 96, s = (e >> 4) % 6, tt = e & 15;
-                const int i = hown + KS * k, ky = a.ky_lo + i, kx = slot_kx(tt, s);
-                const bool in = e < NE && i < a.n_fft_rows && ky * ky + kx * kx <= R * R;
-                float2 pv[KS];
-#pragma unroll
-                for (int p = 0; p < KS; ++p)
-                    pv[p] = in ? cld(ra, PART_OFF + p * kPartElems + (i * 6 + s) * 16 + tt) : make_float2(0.f, 0.f);
-                float2 f = pv[0];
-#pragma unroll
-                for (int p = 1; p < KS; ++p) f = cadd(f, pv[p]);
-                if (e < NE) scr_all[k * XTILE + s * 16 + tt] = f;
-            }
-        }
-        float2 tF = make_float2(0.f, 0.f);
-        if (towner) {
-            float2 pt[KS];
-#pragma unroll
-            for (int p = 0; p < KS; ++p) pt[p] = cld(ra, PART_OFF + p * kPartElems + NROWS * 96 + tid);
-            tF = pt[0];
-#pragma unroll
-            for (int p = 1; p < KS; ++p) tF = cadd(tF, pt[p]);
-        }
-        __syncthreads();  // F of the own rows in the owners' tiles
+        // ---- C: row DFTs of the own rows (full input) -> F (:394)
         float2 F[6];
+        if (g < NOWN) {
 #pragma unroll
-        for (int s = 0; s < 6; ++s) F[s] = scr[s * 16 + t];  // read before the update overwrites the slot
+            for (int m = 0; m < 16; ++m) v[m] = ron ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
+            dft256_out6(v, F, scr, wt, t, xrd);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
+        }
+        // own tail pixels: a 16-lane group sums the 256 columns of the pixel's row
+        for (int pp = g; pp < a.n_tail_px; pp += NG) {
+            if ((tpq[pp] % KS) != hown) continue;  // group-uniform
+            const int2 px = tpx[pp];
+            const int row = NROWS + tpq[pp];
+            pf2 s2p = {0.f, 0.f};
+            pf2 wk = pin(tw[(t * (px.y + NP)) & (NP - 1)]);
+            const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                s2p += pmul(pin(cld(ra, row * NP + t + 16 * m)), wk);
+                if (m < 15) wk = pmul(wk, wstep);
+            }
+            float2 s2 = pout(s2p);
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                s2.x += __shfl_xor(s2.x, o, 64);
+                s2.y += __shfl_xor(s2.y, o, 64);
+            }
+            if (t == 0) tailF[pp] = s2;
+        }
+        __syncthreads();  // tailF
         FPM_STAMP(5)
 
         // ---- object update of the own rows (:405-447), pupil numerator (:457-464)
@@ -496,7 +453,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         if (towner) {
             float oa;
-            const float2 nv = slot_update(tF, Ot, Pt, pm, st, NPt, oa);
+            const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
             cst(rs, wb0 + tp.x * L + tp.y, nv);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
@@ -646,7 +603,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 // ------------------------------------------------------------------ host side
 size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
     const int tld = fz::NP / ks + 1;
-    return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + fz::MAXTAIL) * sizeof(float2) +
+    return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
            (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
