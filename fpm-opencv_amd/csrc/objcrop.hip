@@ -25,6 +25,7 @@
 #include "dft16.hpp"
 #include "dftL.hpp"
 #include "dft200.hpp"
+#include "dft90.hpp"
 #include "fpm_state.hpp"
 
 
@@ -283,15 +284,19 @@ __global__ void __launch_bounds__(64 * W) k_crop_rows600(const float2 *__restric
 // Piece h holds input registers k in [h K, (h + 1) K), K = 20 / NH (element
 // 3 (l + 10 k) + c, 3 l + c < 30, never straddles a piece boundary of a
 // multiple of 30 rows) and the output registers whose rows 10 k + 200 p + l
-// (l < 10) fall in it.  W 8 / NH 4: 48-column strips -- 384-byte row
-// segments, three whole 128-byte lines -- in 59 KB pieces, two blocks per
-// CU (round 2's 12-column strips moved 96-byte segments that straddle lines).
+// (l < 10) fall in it.  The strip moves as 16-byte loads and stores (two
+// columns per thread); the loads of piece h + 2 are issued as soon as piece h
+// has left its registers, so two pieces are in flight while the block works
+// (round 3's version loaded piece by piece with 8-byte loads: 2.4 TB/s, SQ
+// wait_any 0.65 of wave cycles).  W 4 / NH 4: 24-column strips (192-byte row
+// segments, 64-byte aligned), 30 KB pieces.
 // grid (ceil(L / G), B), block 64 W
 template <int W, int NH>
 __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
                                                          float scale, int sy0, int sy1) {
-    constexpr int G = GPW * W, SP = G + 1, HH = L / NH, K = 20 / NH;
+    constexpr int G = GPW * W, SP = G + 1, HH = L / NH, K = 20 / NH, G2 = G / 2;
     static_assert(L % NH == 0 && HH % 30 == 0 && 20 % NH == 0, "pieces of whole 30-row runs");
+    static_assert(L % G == 0 && G % 2 == 0, "whole strips of column pairs");
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     float2 *twL = sm, *tw2 = sm + L, *strip = tw2 + 200;  // HH x SP
     float2 *tiles = strip;  // exchange tiles inside the strip: used only while every column is in registers
@@ -302,29 +307,53 @@ __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io
     const int xrd = opaque_i(l * kXP10);
     load_tw600(twL, tw2, tw_L);
     const int b = blockIdx.y, c0 = blockIdx.x * G;
-    const int ncol = L - c0 < G ? L - c0 : G;
-    const bool colok = act && g < ncol;
     float2 *base = io + (size_t)b * L * L + c0;
-    constexpr int NTH = 64 * W;
+    constexpr int NTH = 64 * W, NLD = (HH * G2 + NTH - 1) / NTH;
+    // objF row y (0 <= y < L) is spec row (y + H) mod L: the live rows of
+    // piece h, [h HH, (h+1) HH), form the contiguous range [ya, yb] relative
+    // to the piece (HH divides H, so a piece never wraps)
+    auto live = [&](int h, int &ya, int &yb) {
+        const int s0 = h * HH >= H ? h * HH - H : h * HH + H;  // spec row of the piece's first row
+        ya = max(sy0 - s0, 0);
+        yb = min(sy1 - s0, HH - 1);
+    };
+    float4 q[2][NLD];
+    auto issue = [&](int h) {
+        int ya, yb;
+        live(h, ya, yb);
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int idx = ya * G2 + threadIdx.x + k * NTH;
+            if (idx < (yb + 1) * G2) {
+                const int y = idx / G2, cc = 2 * (idx - y * G2);
+                q[h & 1][k] = *(const float4 *)(base + (size_t)(y + h * HH) * L + cc);
+            }
+        }
+    };
+    issue(0);
+    issue(1);
     float2 x[3][20];
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
-        // objF row y (0 <= y < L) is spec row (y + H) mod L: the live rows of
-        // this piece [h HH, (h+1) HH) form the contiguous range [ya, yb]
-        // relative to the piece (HH divides H, so a piece never wraps)
-        const int s0 = h * HH >= H ? h * HH - H : h * HH + H;  // spec row of the piece's first row
-        const int ya = max(sy0 - s0, 0), yb = min(sy1 - s0, HH - 1);
-        for (int idx = ya * G + threadIdx.x; idx < (yb + 1) * G; idx += NTH) {
-            const int y = idx / G, cc = idx - y * G;
-            if (cc < ncol) strip[y * SP + cc] = base[(size_t)(y + h * HH) * L + cc];
+        int ya, yb;
+        live(h, ya, yb);
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int idx = ya * G2 + threadIdx.x + k * NTH;
+            if (idx < (yb + 1) * G2) {
+                const int y = idx / G2, cc = 2 * (idx - y * G2);
+                strip[y * SP + cc] = make_float2(q[h & 1][k].x, q[h & 1][k].y);
+                strip[y * SP + cc + 1] = make_float2(q[h & 1][k].z, q[h & 1][k].w);
+            }
         }
+        if (h + 2 < NH) issue(h + 2);
         __syncthreads();
 #pragma unroll
         for (int k = K * h; k < K * h + K; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const int y = 3 * (l + 10 * k) + c - h * HH;
-                x[c][k] = (colok && y >= ya && y <= yb) ? strip[y * SP + g] : make_float2(0.f, 0.f);
+                x[c][k] = (act && y >= ya && y <= yb) ? strip[y * SP + g] : make_float2(0.f, 0.f);
             }
         __syncthreads();
     }
@@ -332,7 +361,7 @@ __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
         __syncthreads();  // exchange tiles / previous piece's reads are done
-        if (colok) {
+        if (act) {
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -341,9 +370,11 @@ __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io
                         strip[(l + 10 * k + 200 * p - h * HH) * SP + g] = cscale(x[p][k], scale);
         }
         __syncthreads();
-        for (int idx = threadIdx.x; idx < HH * G; idx += NTH) {
-            const int y = idx / G, cc = idx - y * G;
-            if (cc < ncol) base[(size_t)(y + h * HH) * L + cc] = strip[y * SP + cc];
+#pragma unroll 4
+        for (int idx = threadIdx.x; idx < HH * G2; idx += NTH) {
+            const int y = idx / G2, cc = 2 * (idx - y * G2);
+            const float2 p0 = strip[y * SP + cc], p1 = strip[y * SP + cc + 1];
+            *(float4 *)(base + (size_t)(y + h * HH) * L + cc) = make_float4(p0.x, p0.y, p1.x, p1.y);
         }
     }
 }
@@ -372,19 +403,182 @@ hipError_t launch_crop600(const DevState &st, float2 *out, const float2 *tw_L, h
 }
 }  // namespace c600
 
+// ------------------------------------------------------------ L = 360 (= 90 x 4)
+// BASELINE configs 1 and 2 (dataset_mono: Np 90, resImprovementFactor 4).
+// One 360-point transform per 10-lane group (dft90.hpp, six groups per wave,
+// lanes 60..63 idle): x[i], i = 4 m + c (c < 4, m < 90): Y_c = DFT90 of
+// x[4 m + c], lane l holding m = l + 10 k (layout A, k < 9), which dft90_ab
+// leaves in layout B (lane j < 9 holds Y_c[j + 9 k'], k' < 10); the radix-4
+// combine X[k + 90 p] = sum_c W360^{c k} W4^{c p} Y_c[k], k = j + 9 k', is
+// lane-local.  The element roll of fftShift (L/2 = 180 = 4 x 45) is not a
+// register relabel here, so pass 1 gathers each element from its rolled
+// source column.  (Round 3 ran L 360 on the mixed-radix k_fft_batch: full
+// rows and columns, 0.15 ms per step at config 2.)
+namespace c360 {
+constexpr int L = 360, H = 180, GPW = 6;
+
+// x[c][k] = element 4 (l + 10 k) + c (k < 9; x[c][9] scratch); on return
+// x[p][k'] = X[j + 9 k' + 90 p] on lanes j < 9
+template <bool INV>
+__device__ __forceinline__ void dft360_regs(float2 (&x)[4][10], float2 *tile, const float2 *tw90, const float2 *twL,
+                                            int l, int xrd) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dft90_ab<INV>(x[c], tile, tw90, l, xrd);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        const int kk = (l < 9 ? l : 0) + 9 * k;
+        float2 z[4];
+        z[0] = x[0][k];
+#pragma unroll
+        for (int c = 1; c < 4; ++c) {
+            const pf2 w = pin(twL[c * kk]);  // c kk < 270 < L
+            z[c] = pout(INV ? pmulc(pin(x[c][k]), w) : pmul(pin(x[c][k]), w));
+        }
+        dft4<INV>(z);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) x[p][k] = z[p];
+    }
+}
+
+// W360 table and tw90[a * 10 + b] = W90^{a b} = W360^{4 a b}
+__device__ __forceinline__ void load_tw360(float2 *twL, float2 *tw90, const float2 *__restrict__ tw_L) {
+    for (int i = threadIdx.x; i < L; i += blockDim.x) twL[i] = tw_L[i];
+    for (int i = threadIdx.x; i < 100; i += blockDim.x) tw90[i] = tw_L[(4 * (i / 10) * (i % 10)) % L];
+    __syncthreads();
+}
+
+// objF row / column i holds spec row / column (i + H) mod L
+__device__ __forceinline__ int roll360(int i) { return i + H < L ? i + H : i - H; }
+
+// pass 1: row IDFTs of the live spectrum rows.  grid (ceil(nlive / (6 W)), B), block 64 W
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_crop_rows360(const float2 *__restrict__ spec, float2 *__restrict__ out,
+                                                         const float2 *__restrict__ tw_L, int sy0, int sy1, int sx0,
+                                                         int sx1) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2 *twL = sm, *tw90 = sm + L, *tiles = tw90 + 100;  // 6 W exchange tiles of 100 + a dummy
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gw = lane / 10;
+    const bool act = gw < GPW;
+    const int l = act ? lane - 10 * gw : 0, g = w * GPW + (act ? gw : 0);
+    float2 *tile = tiles + (act ? g : GPW * W) * 100;
+    const int xrd = opaque_i(l * kXP90);
+    load_tw360(twL, tw90, tw_L);
+    const int b = blockIdx.y, srow = sy0 + blockIdx.x * GPW * W + g;
+    const bool live = act && srow <= sy1;
+    const float2 *src = spec + (size_t)b * L * L + (size_t)(srow <= sy1 ? srow : sy1) * L;
+    float2 x[4][10];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int sc = roll360(4 * (l + 10 * k) + c);  // objF element i <- spec column (i + H) mod L
+            x[c][k] = in_band(sc, sx0, sx1) ? src[sc] : make_float2(0.f, 0.f);
+        }
+    dft360_regs<true>(x, tile, tw90, twL, l, xrd);
+    if (!live || l >= 9) return;
+    float2 *dst = out + (size_t)b * L * L + (size_t)roll360(srow) * L;  // objF row = spec row + L/2
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int k = 0; k < 10; ++k) dst[l + 9 * k + 90 * p] = x[p][k];
+}
+
+// pass 2: column IDFTs in place, scaled 1/L^2, one strip of G = 6 W columns
+// per block through LDS in one piece (L x (G + 1) complex: 72 KB at W 4, two
+// blocks per CU), 16-byte loads and stores.  Rows of the intermediate outside
+// the live band were not written by pass 1 and are read as zero.
+// grid (L / G, B), block 64 W
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_crop_cols360(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
+                                                         float scale, int sy0, int sy1) {
+    constexpr int G = GPW * W, SP = G + 1, G2 = G / 2, NTH = 64 * W;
+    static_assert(L % G == 0 && G % 2 == 0, "whole strips of column pairs");
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    float2 *twL = sm, *tw90 = sm + L, *strip = tw90 + 100;  // L x SP
+    float2 *tiles = strip;  // exchange tiles inside the strip: used only while every column is in registers
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gw = lane / 10;
+    const bool act = gw < GPW;
+    const int l = act ? lane - 10 * gw : 0, g = w * GPW + (act ? gw : 0);
+    float2 *tile = tiles + (act ? g : G) * 100;
+    const int xrd = opaque_i(l * kXP90);
+    load_tw360(twL, tw90, tw_L);
+    const int b = blockIdx.y, c0 = blockIdx.x * G;
+    float2 *base = io + (size_t)b * L * L + c0;
+    auto live = [&](int y) { return in_band(roll360(y), sy0, sy1); };
+    // live objF rows: [0, sy1 - H] and [sy0 + H, L) when the band straddles
+    // the spectrum's middle row, [sy0 - H, sy1 - H] or [sy0 + H, sy1 + H] otherwise
+    for (int idx = threadIdx.x; idx < L * G2; idx += NTH) {
+        const int y = idx / G2, cc = 2 * (idx - y * G2);
+        if (live(y)) {
+            const float4 q = *(const float4 *)(base + (size_t)y * L + cc);
+            strip[y * SP + cc] = make_float2(q.x, q.y);
+            strip[y * SP + cc + 1] = make_float2(q.z, q.w);
+        }
+    }
+    __syncthreads();
+    float2 x[4][10];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int y = 4 * (l + 10 * k) + c;
+            x[c][k] = (act && live(y)) ? strip[y * SP + g] : make_float2(0.f, 0.f);
+        }
+    __syncthreads();
+    dft360_regs<true>(x, tile, tw90, twL, l, xrd);
+    __syncthreads();  // exchange tiles are done before the strip is rewritten
+    if (act && l < 9) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) strip[(l + 9 * k + 90 * p) * SP + g] = cscale(x[p][k], scale);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int idx = threadIdx.x; idx < L * G2; idx += NTH) {
+        const int y = idx / G2, cc = 2 * (idx - y * G2);
+        const float2 p0 = strip[y * SP + cc], p1 = strip[y * SP + cc + 1];
+        *(float4 *)(base + (size_t)y * L + cc) = make_float4(p0.x, p0.y, p1.x, p1.y);
+    }
+}
+
+template <int WR, int WC>
+hipError_t launch_crop360(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
+    constexpr int GC = GPW * WC;
+    const size_t lds_rows = (size_t)(L + 100 + (GPW * WR + 1) * 100) * sizeof(float2);
+    constexpr size_t strip = (size_t)L * (GC + 1) > (size_t)(GC + 1) * 100 ? (size_t)L * (GC + 1) : (size_t)(GC + 1) * 100;
+    const size_t lds_cols = (L + 100 + strip) * sizeof(float2);
+    hipError_t e = hipFuncSetAttribute((const void *)k_crop_rows360<WR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds_rows);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_crop_cols360<WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_cols);
+    if (e != hipSuccess) return e;
+    if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1)
+        return hipErrorInvalidValue;
+    const int nrows = st.sy1 - st.sy0 + 1, gr = GPW * WR;
+    hipLaunchKernelGGL(k_crop_rows360<WR>, dim3((nrows + gr - 1) / gr, st.B), dim3(64 * WR), lds_rows, s,
+                       (const float2 *)st.spec, out, tw_L, st.sy0, st.sy1, st.sx0, st.sx1);
+    hipLaunchKernelGGL(k_crop_cols360<WC>, dim3(L / GC, st.B), dim3(64 * WC), lds_cols, s, out, tw_L,
+                       1.0f / ((float)L * (float)L), st.sy0, st.sy1);
+    return hipGetLastError();
+}
+}  // namespace c360
+
 }  // namespace
 
 constexpr int kCropG = 16;   // columns per strip: 128-byte row segments
 constexpr int kCropGR = 4;   // rows per block in the row pass
 
-// hipErrorNotSupported when L is not 512 / 768 / 1024 / 600 (caller falls back to
+// hipErrorNotSupported when L is not 512 / 768 / 1024 / 600 / 360 (caller falls back to
 // the mixed-radix batched transform)
 hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
     switch (st.L) {
         case 512: return launch_crop<2, kCropGR, kCropG>(st, out, tw_L, s);
         case 768: return launch_crop<3, kCropGR, kCropG>(st, out, tw_L, s);
         case 1024: return launch_crop<4, kCropGR, kCropG>(st, out, tw_L, s);
-        case 600: return c600::launch_crop600<1, 8, 4>(st, out, tw_L, s);
+        case 600: return c600::launch_crop600<1, 4, 4>(st, out, tw_L, s);
+        case 360: return c360::launch_crop360<1, 4>(st, out, tw_L, s);
         default: return hipErrorNotSupported;
     }
 }

@@ -220,14 +220,16 @@ def test_wave_and_tiled_column_passes_agree(Np, L, r, monkeypatch):
         assert rel_l2(wave["pupil"][b], tiled["pupil"][b]) < 2e-6
 
 
-@pytest.mark.parametrize("L,step", [(512, 60), (768, 100), (1024, 150)])
-def test_objcrop_live_band(L, step):
+@pytest.mark.parametrize("Np,L,step", [(256, 512, 60), (256, 768, 100), (256, 1024, 150), (200, 600, 80),
+                                       (90, 360, 40)])
+def test_objcrop_live_band(Np, L, step):
     """objCrop transforms only the live band of the spectrum (rows/columns the
     init placement and the used LEDs' support boxes reach, fpm_state.hpp):
     with an LED set off to one side the band is asymmetric, the spectrum is
     exactly zero outside it, and objCrop still equals the dense IDFT of objF
     (numpy, complex128) computed from the GPU's own spectrum."""
-    Np, r = 256, 33
+    # L 600 / 360: the Np 200 / Np 90 kernels and the 600- / 360-point objCrop passes
+    r = {256: 33, 200: 26, 90: 30}[Np]
     c = L // 2 - Np // 2
     x0 = np.array([c, c + step, c + 2 * step, c + step])
     y0 = np.array([c, c, c - step, c - 2 * step])
