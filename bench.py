@@ -161,7 +161,7 @@ def load_pmc(path, kernel):
 
 def kernel_name(info):
     """Name of the LED-update kernel the context launches (rocprof / pmc key):
-    the template instance for the Np 256 kernel (workgroups per patch)."""
+    the template instance (workgroups per patch) for the Np 256 kernels."""
     import fpm_amd
     if info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256:
         return f"k_fused_iteration<512,{info.wg_per_patch}>"

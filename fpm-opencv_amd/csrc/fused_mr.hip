@@ -53,14 +53,21 @@ constexpr int NW = NT / 64;
 constexpr int NG = NW * GPW;              // 72 groups >= box rows (r <= 35)
 constexpr int SK[6] = {0, 1, 2, 17, 18, 19};  // registers that can hold |k| <= 29
 constexpr int RMAX = 29;
+static_assert(NG >= 2 * RMAX + 1, "one group per box row");
 constexpr int KYOFF = 32;                 // sig table covers ky in [-32, 31]
 constexpr int XP = 10;                    // exchange-tile row pitch (complex)
 constexpr int XT = 10 * XP;               // exchange tile per group (complex)
-// Group stride of the exchange tiles when LDS allows (r <= 28): 106 = 10 (mod
-// 32), so the 8-byte row writes of the three groups a 32-lane LDS batch holds
-// land on disjoint banks (106 * 2 dwords = 20 mod 64); with stride 100 they
-// overlapped two ways (the 16-byte row reads stay conflict-free either way).
-constexpr int kXtFast = 106;
+// Exchange-tile layouts, per wave slot (six group tiles of 100 complex):
+//   dense   stride 100 (slot 600)
+//   stride  106 = 10 (mod 32): the 8-byte row writes of the groups sharing a
+//           16-lane batch land on disjoint banks (slot 636)
+//   shifted the s90 kernel's offsets 0, 122, 230, 356, 478, 602 (slot 704;
+//           fused_s90.hip): writes and 16-byte row reads both spread
+//           (tools/lds_s90.py: 80 LDS cycles per exchange round vs 90 with
+//           stride 106 and 60 conflict-free)
+// The largest that fits with the T pitch below is used.
+constexpr int XW_DENSE = 600, XW_STRIDE = 636, XW_SHIFT = 704;
+constexpr int XG_SHIFT[GPW] = {0, 122, 230, 356, 478, 602};
 constexpr int TLD = NP + 1;               // T row pitch (complex), dense
 // T row pitch when LDS allows: 202 = 10 (mod 32), so the column reads of
 // pass B (consecutive rows for the ten lanes of a group, adjacent columns for
@@ -79,7 +86,8 @@ struct FusedMRArgs {
     int btx0, bty0, nbx, nbt;  // live-band tiles (fpm_fused.hip FusedArgs)
     float rnbx;
     unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles, else null
-    int xt;                    // exchange-tile stride per group (complex): kXtFast or fm::XT
+    int xw;                    // exchange tiles: wave slot (complex)
+    int xg[fm::GPW];           // tile offset of group gw in the wave slot
     int tld;                   // T row pitch (complex): TLD_FAST or fm::TLD
 };
 
@@ -94,7 +102,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *tiles = sm;                        // NG * XT exchange tiles
     const int TLD = a.tld;
-    float2 *th = tiles + NG * a.xt;            // (NB + 2) * TLD: T rows, zero row, dummy row
+    float2 *th = tiles + NW * a.xw;            // (NB + 2) * TLD: T rows, zero row, dummy row
     float2 *tw2 = th + (NB + 2) * TLD;         // [m1][l] = W200^{l m1}
     float *red = (float *)(tw2 + 200);         // 48
     int *sig = (int *)(red + 48);              // 64: T row of ky in [-32, 31], -1 outside the box
@@ -108,7 +116,10 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     const int l = act ? lane - N2 * gw : 0;    // lane within the group
     const int g = w * GPW + (act ? gw : 0);    // group in the workgroup
     const int b = blockIdx.x;
-    float2 *tile = tiles + g * a.xt;
+    int xgo = a.xg[0];  // group offset (uniform kernel-argument values, selected per lane)
+#pragma unroll
+    for (int i = 1; i < GPW; ++i) xgo = gw == i ? a.xg[i] : xgo;
+    float2 *tile = tiles + w * a.xw + xgo;
     const int xrd = opaque_i(l * XP);
     const int nwords = (a.nbt + 31) >> 5;
 
@@ -396,8 +407,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 
 // ------------------------------------------------------------------ host side
 namespace {
-size_t mr_lds_bytes(int nb, int nbt, int xt = fm::XT, int tld = fm::TLD) {
-    return (size_t)(fm::NG * xt + (nb + 2) * tld + 200) * sizeof(float2) + 48 * sizeof(float) +
+size_t mr_lds_bytes(int nb, int nbt, int xw = fm::XW_DENSE, int tld = fm::TLD) {
+    return (size_t)(fm::NW * xw + (nb + 2) * tld + 200) * sizeof(float2) + 48 * sizeof(float) +
            64 * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) +
            sizeof(int);
 }
@@ -434,9 +445,12 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
     // bank-friendly strides while LDS allows: tiles first, then the T pitch
     // (FPM_MR_DENSE=1 forces the dense layout, test_gpu_fused_mr.py)
     const bool dense = getenv("FPM_MR_DENSE") != nullptr;
-    a.xt = !dense && mr_lds_bytes(st.nb, a.nbt, fm::kXtFast) <= 160 * 1024 ? fm::kXtFast : fm::XT;
-    a.tld = !dense && mr_lds_bytes(st.nb, a.nbt, a.xt, fm::TLD_FAST) <= 160 * 1024 ? fm::TLD_FAST : fm::TLD;
-    const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xt, a.tld);
+    auto fits = [&](int xw, int tld) { return !dense && mr_lds_bytes(st.nb, a.nbt, xw, tld) <= 160 * 1024; };
+    a.tld = fits(fm::XW_STRIDE, fm::TLD_FAST) ? fm::TLD_FAST : fm::TLD;
+    a.xw = fits(fm::XW_SHIFT, a.tld) ? fm::XW_SHIFT : fits(fm::XW_STRIDE, a.tld) ? fm::XW_STRIDE : fm::XW_DENSE;
+    for (int i = 0; i < fm::GPW; ++i)
+        a.xg[i] = a.xw == fm::XW_SHIFT ? fm::XG_SHIFT[i] : i * (a.xw == fm::XW_STRIDE ? 106 : fm::XT);
+    const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xw, a.tld);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_mr, dim3(st.B), dim3(fm::NT), lds, s, a);

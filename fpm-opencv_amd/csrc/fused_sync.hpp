@@ -98,4 +98,23 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Plain launch of a grid whose workgroups wait on each other (split and
+// distributed modes): every block must be resident at once.  The grid is
+// checked against the occupancy query -- the check hipLaunchCooperativeKernel
+// makes -- and launched plainly: the same residency (MI355X_MICROARCH.md
+// "coop-launch") without the cooperative launch's per-launch host cost.  Every
+// wait in those kernels also gives up after ~1 s and raises the sticky abort
+// word, so a grid that could not be co-resident fails instead of hanging.
+template <class Args>
+inline hipError_t launch_coresident(const void *fn, int grid, int block, size_t lds, Args *a, hipStream_t s) {
+    int dev = 0, n_cu = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
+    if (e != hipSuccess) return e;
+    if ((long long)per_cu * n_cu < grid) return hipErrorCooperativeLaunchTooLarge;
+    void *args[] = {a};
+    return hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s);
+}
+
 }  // namespace fpm

@@ -16,10 +16,11 @@ fi
 IFS=';' read -ra WL <<< "${WORKLOADS:-metric:}"
 for i in $(seq 1 ${REPS:-2}); do
   for W in "${WL[@]}"; do
-    N=${W%%:*}; A=${W#*:}
+    N=${W%%:*}; A=${W#*:}; E=FPM_AB_NONE=1
+    case "$A" in FPM_*) E=${A%% *}; A=${A#* };; esac  # "name:FPM_X=1 --args": an environment setting for both
     for V in cur $VAR; do
       if [ $V = cur ]; then unset FPM_HIP_LIB; else export FPM_HIP_LIB=$GRAFT_REPO_ROOT/fpm-opencv_amd/lib_$V/libfpm_hip.so; fi
-      timeout -k 10 300 python bench.py --no-cpu-baseline --no-gather $A > $O/${N}_$V$i.json 2> $O/${N}_$V$i.err || { echo "$N $V rc=$?"; tail -3 $O/${N}_$V$i.err; exit 1; }
+      env $E timeout -k 10 300 python bench.py --no-cpu-baseline --no-gather $A > $O/${N}_$V$i.json 2> $O/${N}_$V$i.err || { echo "$N $V rc=$?"; tail -3 $O/${N}_$V$i.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/${N}_$V$i.json')); print('$N $V', d['value'], d['ms_per_step'], d['led_ms_per_step'], d['objcrop_ms_per_step'], d['config']['kernel'])"
     done
   done

@@ -43,9 +43,10 @@ N_SIMD = 1024
 
 
 def short(name):
-    """Kernel key: the Np 256 fused kernel keeps its template instance
-    (k_fused_iteration<NT,KS>: threads, workgroups per patch) so a profile of
-    the split-mode instance is never read as the one-workgroup kernel's."""
+    """Kernel key: the Np 256 fused kernels keep their template instance
+    (k_fused_iteration<NT,KS>, k_fused_dist<KS>: workgroups per patch) so a
+    profile of a split-mode instance is never read as the one-workgroup
+    kernel's."""
     import re
     m = re.search(r"k_fused_iteration<(\d+),\s*(\d+)>", name)
     if m:
