@@ -31,6 +31,8 @@
 
 namespace fpm {
 
+typedef float f32x4_nt __attribute__((ext_vector_type(4)));
+
 namespace {
 
 // live-band test: a <= i <= b
@@ -176,7 +178,9 @@ __global__ void __launch_bounds__(16 * G) k_crop_cols(float2 *__restrict__ io, c
         for (int idx = threadIdx.x; idx < H * G / 2; idx += NTH) {
             const int y = idx / (G / 2), cc = 2 * (idx - y * (G / 2));
             const float2 p0 = strip[y * SP + cc], p1 = strip[y * SP + cc + 1];
-            *(float4 *)(base + (size_t)(y + h * H) * L + cc) = make_float4(p0.x, p0.y, p1.x, p1.y);
+            // the output is not re-read: non-temporal stores (0.584 -> 0.569 ms
+            // per step at L 768; the 600-point pass measured 1 % slower with them)
+            __builtin_nontemporal_store((f32x4_nt){p0.x, p0.y, p1.x, p1.y}, (f32x4_nt *)(base + (size_t)(y + h * H) * L + cc));
         }
     }
 }
