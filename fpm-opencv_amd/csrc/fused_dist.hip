@@ -270,10 +270,12 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 for (int m = 0; m < 16; ++m) cst(ra, irow * NP + t + 16 * m, r[m]);
             }
         }
-        // own tail rows: direct sums over the row's pixels for every column x
+        // own tail rows: direct sums over the row's pixels for every column x,
+        // on the LAST waves (the FFT-row groups g < NOWN sit in the first
+        // waves, so at KS 4 / 8 the sums run beside the row IDFTs)
         for (int q = hown; q < a.n_tail_rows; q += KS) {
             const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
-            for (int x = tid; x < NP; x += NT) {
+            for (int x = NT - 1 - tid; x < NP; x += NT) {
                 const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
                 pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
                 const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
@@ -407,8 +409,12 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 #pragma unroll
             for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
         }
-        // own tail pixels: a 16-lane group sums the 256 columns of the pixel's row
-        for (int pp = g; pp < a.n_tail_px; pp += NG) {
+        // own tail pixels: a 16-lane group sums the 256 columns of the pixel's
+        // row; pixels go to the last groups first, which own no FFT row at
+        // KS 4 / 8, so the sums overlap the row DFTs instead of following them
+        // on the same groups (round 3: C 7.5k cycles per LED on the parts
+        // that own a tail row vs 3.2k on the part that owns none, at KS 4)
+        for (int pp = NG - 1 - g; pp < a.n_tail_px; pp += NG) {
             if ((tpq[pp] % KS) != hown) continue;  // group-uniform
             const int2 px = tpx[pp];
             const int row = NROWS + tpq[pp];
