@@ -158,9 +158,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         roff[s] = sg >= 0 ? sg * TLD : zoff;
     }
     for (int i = tid; i < TLD; i += NT) th[zoff + i] = make_float2(0.f, 0.f);
-    // tail pixel tid: this part owns it when its row q = tpq[tid] is q = hown (mod KS)
-    const bool towner = tid < a.n_tail_px && (tpq[tid] % KS) == hown;
-    const int2 tp = tid < a.n_tail_px ? tpx[tid] : make_int2(0, 0);
+    // tail pixel ti: this part owns it when its row q = tpq[ti] is q = hown
+    // (mod KS).  At KS 8 thread NT - 1 - ti (the last wave, which owns no FFT
+    // row: the tail updates and window-tile merges run beside the row
+    // updates) -- 32-patch shard +1.2 %; at KS 4 the first wave measured
+    // 0.6 % faster (profiles/r04_ab/dist_lastwave_ab.txt)
+    const int ti = KS == 8 ? NT - 1 - tid : tid;
+    const bool towner = ti < a.n_tail_px && (tpq[ti] % KS) == hown;
+    const int2 tp = ti < a.n_tail_px ? tpx[ti] : make_int2(0, 0);
     float2 Pt = towner ? pup[(tp.x + R) * NB + tp.y + R] : make_float2(0.f, 0.f);
     float2 NPt = make_float2(0.f, 0.f), Ot = make_float2(0.f, 0.f);
     float pm = st.pmax[b];
@@ -256,7 +261,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         float2 v[16], r[16];
 
         // ---- gather + A: row IDFTs of the own rows, all 256 outputs to Tg (:358-365)
-        if (towner) tailX[tid] = pout(pmul(pin(Ot), pin(Pt)));
+        if (towner) tailX[ti] = pout(pmul(pin(Ot), pin(Pt)));
         __syncthreads();  // tailX
         FPM_STAMP(0)
         if (g < NOWN) {  // group-uniform
@@ -459,7 +464,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         if (towner) {
             float oa;
-            const float2 nv = slot_update(tailF[tid], Ot, Pt, pm, st, NPt, oa);
+            const float2 nv = slot_update(tailF[ti], Ot, Pt, pm, st, NPt, oa);
             cst(rs, wb0 + tp.x * L + tp.y, nv);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
@@ -471,9 +476,10 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             const int dy = k / wnx;
             return (wty0 + dy - a.bty0) * a.nbx + (wtx0 + k - dy * wnx - a.btx0);
         };
-        if (tid < wnt) {
-            const int bk = wtile(tid);
-            cst(ra, TILES_OFF + hown * kWinTiles + tid,
+        // window tiles: thread ti handles tile ti (see towner)
+        if (ti < wnt) {
+            const int bk = wtile(ti);
+            cst(ra, TILES_OFF + hown * kWinTiles + ti,
                 make_float2(tmx[bk], __uint_as_float((dirty[bk >> 5] >> (bk & 31)) & 1u)));
         }
         FPM_STAMP(6)
@@ -485,14 +491,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // the next window first (its loads overlap the merge), then the
         // merge: every part ends with the same maxima and dirty bits
         if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
-        if (tid < wnt) {
-            const int bk = wtile(tid);
+        if (ti < wnt) {
+            const int bk = wtile(ti);
             float m = tmx[bk];
             unsigned d = 0;
 #pragma unroll
             for (int p = 0; p < KS; ++p) {
                 if (p == hown) continue;
-                const float2 e = cld(ra, TILES_OFF + p * kWinTiles + tid);
+                const float2 e = cld(ra, TILES_OFF + p * kWinTiles + ti);
                 m = fmaxf(m, e.x);
                 d |= __float_as_uint(e.y);
             }
