@@ -17,17 +17,26 @@ CONFIG = {"metric": "metric", "c2": "c2", "c3": "c3", "c5": "c5", "pt128": "metr
           "pt32": "metric"}
 
 
+def led_kernel(pmc):
+    """The workload's LED-update kernel key in a counter file (bench.py
+    kernel_name): the fused kernel profiled, or the general path's LED step."""
+    keys = json.load(open(pmc))["per_launch_hbm_bytes"].keys()
+    fused = [k for k in keys if k.startswith("k_fused")]
+    return fused[0] if len(fused) == 1 else "general_led_step"
+
+
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
     for w, cfg in CONFIG.items():
         b = os.path.join(src, f"bench_{w}.json")
-        if not os.path.exists(b):
-            continue
-        shutil.copy(b, os.path.join(prof, f"{rnd}_bench_{w}.json"))
-        kern = json.load(open(b))["config"]["kernel"]
         pmc = os.path.join(src, f"pmc_{w}", "pmc.json")
+        if os.path.exists(b):
+            shutil.copy(b, os.path.join(prof, f"{rnd}_bench_{w}.json"))
         if os.path.exists(pmc):
+            # the counter run of an evidence part may come without its bench
+            # line (tools/gpu/r04_prof.sh runs in parts): key from the file
+            kern = json.load(open(b))["config"]["kernel"] if os.path.exists(b) else led_kernel(pmc)
             k = kern.replace("<", "_").replace(">", "").replace(",", "_")
             shutil.copy(pmc, os.path.join(prof, f"pmc_{cfg}_{k}.json"))
             s = os.path.join(src, f"pmc_{w}", "pmc_summary.txt")

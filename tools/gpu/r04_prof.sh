@@ -4,6 +4,10 @@
 # every workload reading those fresh counter files (--pmc), the kernel-trace
 # stats of the headline command, and phase stamps of the shard workloads.
 # tools/collect_profiles.py gpurun_out/<TAG> r04 copies the results to profiles/.
+# A GPU call is limited to 20 minutes, so the run comes in parts:
+#   PMC="metric pt128 pt64" (counter passes of these workloads only; SKIP_TESTS=1 skips the suite)
+#   BENCH=1 SKIP_TESTS=1 SKIP_PMC=1 (bench lines reading the collected profiles/pmc_* files,
+#   kernel trace, stamps)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -21,6 +25,7 @@ W_ALL="metric: c2:--config_c2 c3:--config_c3 c5:--config_c5 pt128:--patches-tota
 if [ -z "$SKIP_PMC" ]; then
   for W in $W_ALL; do
     N=${W%%:*}; A=${W#*:}
+    case " ${PMC:-metric c2 c3 c5 pt128 pt64 pt32} " in *" $N "*) ;; *) continue;; esac
     TAG=$T/pmc_$N BENCH_ARGS="${A//_/ }" bash tools/gpu/prof_counters.sh || { echo "pmc $N failed"; exit 1; }
     echo "pmc $N done"
   done
@@ -29,6 +34,7 @@ bl() {  # name, args
   timeout -k 10 400 python bench.py $2 > $O/bench_$1.json 2> $O/bench_$1.err || { echo "BENCH $1 rc=$?"; tail -3 $O/bench_$1.err; return 1; }
   python3 -c "import json; d=json.load(open('$O/bench_$1.json')); r=d['roofline']; print('$1', d['value'], d['ms_per_step'], d['led_ms_per_step'], d['objcrop_ms_per_step'], r['kernel'], r['frac'], r['hbm']['frac'], r.get('traffic'))"
 }
+[ -z "$BENCH" ] && { echo "evidence part done"; exit 0; }
 pm() { [ -f $O/pmc_$1/pmc.json ] && echo "--pmc $O/pmc_$1/pmc.json"; }
 bl metric "--steps 20 --warmup 5 $(pm metric)" && \
 bl c2 "--config c2 --steps 20 --warmup 3 --no-cpu-baseline $(pm c2)" && \
