@@ -756,11 +756,19 @@ __global__ void k_init_place(DevState st, const float2 *__restrict__ F, size_t f
     if (row == 0 && threadIdx.x == 0) st.pmax[b * st.npart] = (st.disk[r * nb + r] ? 1.f : 0.f);
 }
 
-// tile maxima of |spec| from scratch. grid (ntx*nty, B), block 256
+// tile maxima of |spec| after k_init_place. grid (ntx*nty, B), block 256.
+// The spectrum was just zeroed except the init box [L/2 - r, L/2 + r]^2, so a
+// tile outside it is 0 without reading it (init read the whole spectrum
+// again: 1.2 GB at the metric config)
 __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
     __shared__ float red[8];
     const int t = blockIdx.x, b = blockIdx.y, L = st.L;
     const int ty = t / st.ntx, tx = t % st.ntx;
+    const int lo = L / 2 - st.r, hi = L / 2 + st.r;
+    if (ty * kTile > hi || ty * kTile + kTile - 1 < lo || tx * kTile > hi || tx * kTile + kTile - 1 < lo) {
+        if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = 0.f;  // block-uniform
+        return;
+    }
     const int y = ty * kTile + (threadIdx.x >> 4), x = tx * kTile + (threadIdx.x & 15);
     float m = 0.f;
     if (y < L && x < L) m = cmag(spec_ld(st, b, (size_t)y * L + x));
@@ -768,7 +776,7 @@ __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
     if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = m;
 }
 
-// row maxima of the tile maxima from scratch (general path). grid (nty, B)
+// row maxima of the tile maxima after init (general path). grid (nty, B)
 __global__ void __launch_bounds__(256) k_row_max_all(DevState st) {
     __shared__ float red[4];
     const int ty = blockIdx.x, b = blockIdx.y;
