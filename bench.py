@@ -451,12 +451,7 @@ def main():
     value = updates / elapsed
     per_launch_ms = led_ms / max(launches, 1)
     fused = info.path == fpm_amd.PATH_FUSED
-    if fused:
-        per_launch_updates = B * geo["n_led"]
-    elif info.fused_kernel == fpm_amd.KERNEL_CHAIN_NP1024:  # one launch per 8 patches per iteration
-        per_launch_updates = B * geo["n_led"] / ((B + 7) // 8)
-    else:  # the general path's per-LED launches
-        per_launch_updates = B
+    per_launch_updates = B * geo["n_led"] if fused else B
     roofline = roofline_line(geo, info, per_launch_ms, per_launch_updates, args.pmc or default_pmc(args, info))
 
     gather = None

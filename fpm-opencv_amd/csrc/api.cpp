@@ -52,10 +52,6 @@ hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas
                                         const FftPlan &pl, unsigned long long *dbg, hipStream_t s);
 // Np 1024 register row/column kernels of the general path (np1024.hip)
 bool np1024_supported(int np, int r);
-int np1024_chain_flag_words();
-int np1024_chain_parts(const DevState &st);
-hipError_t launch_np1024_chain(const DevState &st, const int *order_dev, const int *x0_dev, const int *y0_dev,
-                               int n_order, const float2 *tw, int *flags, int G, hipStream_t s);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   int ks, unsigned long long *dbg, float2 *xch, int *flags, int stall_led,
@@ -153,9 +149,6 @@ struct fpm_ctx {
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
-    int chain_g = 0;                // general path, Np 1024: the persistent chain kernel (np1024.hip
-                                    // k_chain1024) with chain_g workgroups per patch; 0 = per-LED kernels
-    int *chain_flags = nullptr;     //   barrier words + XCC ids + sticky abort word
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -413,19 +406,8 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         // two for the Np 1024 kernels, whose row launches cover a few patches
         // in 1.3 rounds of workgroups (config 5, 8 patches: 65.5 -> 57.5 ms of
         // LED steps per iteration; 3 or 4 groups measured slower, 79 / 77 ms)
-        // Np 1024: one persistent launch per iteration (k_chain1024) unless
-        // FPM_NO_CHAIN=1 or the occupancy cannot hold a patch's workgroups
-        if (reg1024 && !getenv("FPM_NO_CHAIN")) {
-            c->chain_g = np1024_chain_parts(st);
-            if (c->chain_g > 0) {
-                const size_t nf = (size_t)np1024_chain_flag_words();
-                if ((rc = dalloc(c, &c->chain_flags, nf))) return fail(rc);
-                if (hipMemset(c->chain_flags, 0, nf * sizeof(int)) != hipSuccess)
-                    return fail(set_err(FPM_ERR_DEVICE, "chain flag init failed"));
-            }
-        }
         const char *pg = getenv("FPM_PATCH_GROUPS");
-        c->ngroups = c->chain_g > 0 ? 1 : pg ? atoi(pg) : (reg1024 ? 2 : 1);
+        c->ngroups = pg ? atoi(pg) : (reg1024 ? 2 : 1);
         c->ngroups = std::max(1, std::min({c->ngroups, B, (int)fpm_ctx::kMaxGroups}));
         for (int g = 1; g < c->ngroups; ++g) {
             if (hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking) != hipSuccess ||
@@ -709,7 +691,7 @@ int fpm_run(fpm_ctx *c, int iters) {
         HIP_TRY(hipEventCreate(&e));
         c->evpool.push_back(e);
     }
-    const bool use_graph = c->path != FPM_PATH_FUSED && c->chain_g == 0 && iters > 0 && !getenv("FPM_NO_GRAPH");
+    const bool use_graph = c->path != FPM_PATH_FUSED && iters > 0 && !getenv("FPM_NO_GRAPH");
     if (use_graph) {
         const int r = general_graph(c);
         if (r != FPM_OK) return r;
@@ -734,9 +716,6 @@ int fpm_run(fpm_ctx *c, int iters) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->split_ks, c->dbg, c->xch,
                                            c->split_flags, c->stall_led, c->stream));
-        } else if (c->chain_g > 0) {
-            HIP_TRY(launch_np1024_chain(c->st, c->order_dev, c->x0_dev, c->y0_dev, c->prob.n_order, c->tw_np,
-                                        c->chain_flags, c->chain_g, c->stream));
         } else if (use_graph) {
             HIP_TRY(launch_general_graphs(c, c->stream));
         } else {
@@ -767,20 +746,6 @@ int fpm_run(fpm_ctx *c, int iters) {
                            "undefined, call fpm_init again", c->split_ks);
         }
     }
-    if (c->chain_flags) {
-        // a chain barrier that timed out (workgroups of a patch not co-resident)
-        int ab = 0;
-        int *abw = c->chain_flags + np1024_chain_flag_words() - 1;
-        HIP_TRY(hipMemcpy(&ab, abw, sizeof(int), hipMemcpyDeviceToHost));
-        if (ab) {
-            HIP_TRY(hipMemset(abw, 0, sizeof(int)));
-            c->initialized = false;
-            c->objcrop_valid = false;
-            return set_err(FPM_ERR_DEVICE,
-                           "chain barrier between the %d workgroups of a patch timed out; results are undefined, "
-                           "call fpm_init again", c->chain_g);
-        }
-    }
     double led_ms = 0, crop_ms = 0;
     for (int it = 0; it < iters; ++it) {
         float a = 0, b = 0;
@@ -794,9 +759,7 @@ int fpm_run(fpm_ctx *c, int iters) {
     c->timing.run_ms = tot;
     c->timing.led_ms = led_ms;
     c->timing.objcrop_ms = crop_ms;
-    c->timing.led_launches = (c->path == FPM_PATH_FUSED) ? iters
-                             : c->chain_g > 0            ? iters * ((c->st.B + 7) / 8)
-                                                         : iters * c->prob.n_order;
+    c->timing.led_launches = (c->path == FPM_PATH_FUSED) ? iters : iters * c->prob.n_order;
     if (c->dbg) {
         unsigned long long h[2 * kStamps];
         HIP_TRY(hipMemcpy(h, c->dbg, sizeof h, hipMemcpyDeviceToHost));
@@ -915,16 +878,14 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
     info->support_px = c->support_px;
     info->device = c->device;
     info->device_bytes = c->bytes;
-    info->wg_per_patch = c->chain_g > 0 ? c->chain_g : c->split_ks;
-    info->fused_kernel = c->chain_g > 0            ? FPM_KERNEL_CHAIN_NP1024
-                         : c->path != FPM_PATH_FUSED ? FPM_KERNEL_GENERAL
+    info->wg_per_patch = c->split_ks;
+    info->fused_kernel = c->path != FPM_PATH_FUSED ? FPM_KERNEL_GENERAL
                          : c->fused_s90        ? FPM_KERNEL_FUSED_NP90
                          : c->fused_small      ? FPM_KERNEL_FUSED_SMALL
                          : c->fused_mr         ? FPM_KERNEL_FUSED_NP200
                          : c->dist             ? FPM_KERNEL_FUSED_NP256_DIST
                                                : FPM_KERNEL_FUSED_NP256;
-    info->threads_per_wg = c->chain_g > 0            ? 512
-                           : c->path != FPM_PATH_FUSED ? 0
+    info->threads_per_wg = c->path != FPM_PATH_FUSED ? 0
                            : c->fused_s90 || c->fused_small ? 1024
                            : c->fused_mr ? 768
                                          : c->fused_nt;

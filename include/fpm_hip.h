@@ -128,9 +128,6 @@ typedef struct fpm_ctx fpm_ctx;
 #define FPM_KERNEL_FUSED_NP256_DIST 4  /* k_fused_dist (Np 256, every phase distributed
                                           over wg_per_patch workgroups; small batches) */
 #define FPM_KERNEL_FUSED_NP90   5  /* k_fused_s90 (Np 90: register 9 x 10 transforms) */
-#define FPM_KERNEL_CHAIN_NP1024 6  /* k_chain1024 (general path, Np 1024: one persistent
-                                      launch per iteration, wg_per_patch workgroups per
-                                      patch; FPM_NO_CHAIN=1 selects the per-LED kernels) */
 
 /* Which path the context runs and its per-launch geometry. */
 typedef struct fpm_info {
@@ -141,8 +138,7 @@ typedef struct fpm_info {
     size_t  device_bytes;  /* device memory owned by the context               */
     int32_t wg_per_patch;  /* fused Np 256 path: workgroups per patch (1, or 2 /
                               4 / 8 in split or distributed mode when
-                              wg_per_patch * n_patch <= CUs); the Np 1024
-                              chain kernel: its workgroups per patch          */
+                              wg_per_patch * n_patch <= CUs)                   */
     int32_t fused_kernel;  /* FPM_KERNEL_*                                      */
     int32_t threads_per_wg;/* threads per workgroup of the LED-update kernel (ABI 4) */
 } fpm_info;

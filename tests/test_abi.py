@@ -66,5 +66,4 @@ def test_flag_and_path_constants_match_header():
     assert {k: int(v) for k, v in kern.items()} == {
         "GENERAL": fpm_amd.KERNEL_GENERAL, "FUSED_NP256": fpm_amd.KERNEL_FUSED_NP256,
         "FUSED_NP200": fpm_amd.KERNEL_FUSED_NP200, "FUSED_SMALL": fpm_amd.KERNEL_FUSED_SMALL,
-        "FUSED_NP256_DIST": fpm_amd.KERNEL_FUSED_NP256_DIST, "FUSED_NP90": fpm_amd.KERNEL_FUSED_NP90,
-        "CHAIN_NP1024": fpm_amd.KERNEL_CHAIN_NP1024}
+        "FUSED_NP256_DIST": fpm_amd.KERNEL_FUSED_NP256_DIST, "FUSED_NP90": fpm_amd.KERNEL_FUSED_NP90}

@@ -21,7 +21,7 @@ def led_kernel(pmc):
     """The workload's LED-update kernel key in a counter file (bench.py
     kernel_name): the fused kernel profiled, or the general path's LED step."""
     keys = json.load(open(pmc))["per_launch_hbm_bytes"].keys()
-    fused = [k for k in keys if k.startswith("k_fused") or k == "k_chain1024"]
+    fused = [k for k in keys if k.startswith("k_fused")]
     return fused[0] if len(fused) == 1 else "general_led_step"
 
 
