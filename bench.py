@@ -161,10 +161,11 @@ def load_pmc(path, kernel):
 
 def kernel_name(info):
     """Name of the LED-update kernel the context launches (rocprof / pmc key):
-    the template instance (workgroups per patch) for the Np 256 kernels."""
+    the template instance (threads and workgroups per patch, fpm_info) for
+    the Np 256 kernels."""
     import fpm_amd
     if info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256:
-        return f"k_fused_iteration<512,{info.wg_per_patch}>"
+        return f"k_fused_iteration<{info.threads_per_wg or 512},{info.wg_per_patch}>"
     if info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256_DIST:
         return f"k_fused_dist<{info.wg_per_patch}>"
     return fpm_amd.KERNEL_NAMES[info.fused_kernel]
