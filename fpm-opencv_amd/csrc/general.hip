@@ -953,6 +953,93 @@ hipError_t launch_init(const DevState &st, int init_led, float2 *scratch, const 
 // rows of the rolled spectrum, then columns, scaled by 1/L^2.
 hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s);
 
+// ---- objCrop for L = 4096 (config 5) ----------------------------------------
+// The batched transform above fits only C = 2 sequences of 4096 points in a
+// block, so its column pass reads 16-byte column segments (the counters:
+// 3x the pass's bytes, 3.6 ms per iteration at config 5).  Here the column
+// IDFT runs first, straight from the (read-only) spectrum, as a six-step
+// 4096 = 64 x 64 transform whose passes read and write 128-byte row segments
+// of 16 adjacent columns; the row IDFT then runs in place on the contiguous
+// rows (the batched transform, element band = the live columns).  With
+// n = n1 + 64 n2 and k = k2 + 64 k1 (inverse, W = e^{+2 pi i / 4096}):
+//   X[k2 + 64 k1] = sum_n1 W64^{n1 k1} [ W^{n1 k2} sum_n2 x[n1 + 64 n2] W64^{n2 k2} ]
+//   pass 1 (block n1): the bracket for all k2, stored at row k2 + 64 n1
+//   pass 2 (block k2): reads rows k2 + 64 n1, writes X at rows k2 + 64 k1 --
+//                      the same rows, so it runs in place
+namespace c4k {
+constexpr int L = 4096, CW = 16, NT = 8 * CW;  // 16 columns x 8 lanes per block
+
+// 64-point inverse DFT of the block's 16 columns, 8 lanes per column (8 x 8:
+// DFT8 over the lane's values, W64 twiddles, LDS exchange, DFT8): lane (c, j)
+// holds x[j + 8 b] in v[b] and returns X[j + 8 q] in v[q].  One barrier; lds
+// is used once per launch.
+__device__ __forceinline__ void idft64(float2 (&v)[8], float2 *lds, int c, int j, const float2 *__restrict__ tw) {
+    dft8<true>(v);  // Z_j[p] = sum_b x[j + 8 b] W8^{b p}
+#pragma unroll
+    for (int p = 1; p < 8; ++p) v[p] = cmul(v[p], cconj(tw[(64 * j * p) & (L - 1)]));  // W64^{j p}
+#pragma unroll
+    for (int p = 0; p < 8; ++p) lds[(c * 8 + j) * 9 + p] = v[p];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 8; ++a) v[a] = lds[(c * 8 + a) * 9 + j];  // Z_a[j]
+    dft8<true>(v);  // X[j + 8 q] = sum_a Z_a[j] W8^{a q}
+}
+
+// pass 1: grid (L / CW, 64 (n1), B); objF row y, column x = spec row / column
+// (y + L/2, x + L/2) mod L; zero outside the live band (fpm_state.hpp)
+__global__ void __launch_bounds__(NT) k_crop4k_cols1(DevState st, float2 *out, const float2 *__restrict__ tw) {
+    __shared__ float2 lds[CW * 8 * 9];
+    const int c = threadIdx.x & (CW - 1), j = threadIdx.x / CW;
+    const int x = blockIdx.x * CW + c, n1 = blockIdx.y, b = blockIdx.z;
+    const int sx = (x + L / 2) & (L - 1);
+    const bool live = sx >= st.sx0 && sx <= st.sx1;
+    float2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int sy = (n1 + 64 * (j + 8 * q) + L / 2) & (L - 1);
+        v[q] = live && sy >= st.sy0 && sy <= st.sy1 ? spec_ld(st, b, (size_t)sy * L + sx) : make_float2(0.f, 0.f);
+    }
+    idft64(v, lds, c, j, tw);
+    float2 *o = out + (size_t)b * L * L + x;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int k2 = j + 8 * q;
+        o[(size_t)(k2 + 64 * n1) * L] = cmul(v[q], cconj(tw[(n1 * k2) & (L - 1)]));  // W^{n1 k2}
+    }
+}
+
+// pass 2: grid (L / CW, 64 (k2), B), in place on out
+__global__ void __launch_bounds__(NT) k_crop4k_cols2(float2 *out, const float2 *__restrict__ tw) {
+    __shared__ float2 lds[CW * 8 * 9];
+    const int c = threadIdx.x & (CW - 1), j = threadIdx.x / CW;
+    const int x = blockIdx.x * CW + c, k2 = blockIdx.y, b = blockIdx.z;
+    float2 *o = out + (size_t)b * L * L + x;
+    float2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = o[(size_t)(k2 + 64 * (j + 8 * q)) * L];
+    idft64(v, lds, c, j, tw);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[(size_t)(k2 + 64 * (j + 8 * q)) * L] = v[q];
+}
+}  // namespace c4k
+
+static hipError_t launch_crop4096(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
+                                  hipStream_t s) {
+    using namespace c4k;
+    const dim3 grid(L / CW, 64, st.B);
+    hipLaunchKernelGGL(k_crop4k_cols1, grid, dim3(NT), 0, s, st, out, tw_L);
+    hipLaunchKernelGGL(k_crop4k_cols2, grid, dim3(NT), 0, s, out, tw_L);
+    // rows in place, scaled by 1/L^2; columns x with spec column (x + L/2) mod L
+    // outside the live band are zero
+    FftBand rows;
+    rows.elo = st.sx0;
+    rows.ehi = st.sx1;
+    rows.eroll = L / 2;
+    const size_t bs = (size_t)L * L;
+    return launch_fft_batch(true, out, out, pl_L, tw_L, L, st.B, bs, L, 1, bs, L, 1, 0, 0,
+                            1.0f / ((float)L * (float)L), s, nullptr, 1.f, rows);
+}
+
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
                           hipStream_t s) {
     // L = 512 / 768 / 1024: register-resident transforms (objcrop.hip)
@@ -960,6 +1047,7 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
         const hipError_t r = launch_objcrop_regs(st, out, tw_L, s);
         if (r != hipErrorNotSupported) return r;
     }
+    if (st.L == c4k::L && !std::getenv("FPM_NO_CROP4K")) return launch_crop4096(st, out, pl_L, tw_L, s);
     const int L = st.L;
     const size_t bs = (size_t)L * L;
     // rows: spec rows (sequences) and columns (elements) outside the live band

@@ -93,3 +93,26 @@ def test_np1024_fp16_scratch_vs_fp32_scratch():
         for b in range(2):
             e = rel_l2(h[k][b], f[k][b])
             assert 0 < e < 2e-3, (k, b, e)
+
+
+@pytest.mark.parametrize("fp16", [False, True], ids=["fp32", "fp16"])
+def test_objcrop_l4096_six_step_equals_batched_transform(fp16):
+    """objCrop at L 4096 (config 5): the six-step column IDFT (64 x 64, two
+    passes of 128-byte row segments, general.hip c4k) then the in-place row
+    IDFT, vs the batched transform rows-then-columns (FPM_NO_CROP4K=1): the
+    same 2-D IDFT in a different order, so within rounding (1e-6 relative L2)."""
+    L, r = 4096, 333
+    x0, y0, order = grid_geometry(Np, L, 2, 600)
+    stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=95)
+    flags = fpm_amd.FLAG_SPEC_FP16 if fp16 else 0
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=1, flags=flags)
+    new = _run(prob, stack, 1)
+    os.environ["FPM_NO_CROP4K"] = "1"
+    try:
+        old = _run(prob, stack, 1)
+    finally:
+        os.environ.pop("FPM_NO_CROP4K", None)
+    np.testing.assert_array_equal(new["objF"][0], old["objF"][0])
+    e = rel_l2(new["objCrop"][0], old["objCrop"][0])
+    print(f"objCrop L 4096 six-step vs batched: rel L2 {e:.2e}")
+    assert e < 1e-6, e
