@@ -1021,23 +1021,49 @@ __global__ void __launch_bounds__(NT) k_crop4k_cols2(float2 *out, const float2 *
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[(size_t)(k2 + 64 * (j + 8 * q)) * L] = v[q];
 }
+
+// rows: grid (L, B), block 512, in place on out: the same 64 x 64 split within
+// the row held by the block -- lane (n1, j) runs the DFT64 over n2 for column
+// n1 of the row's 64 x 64 matrix x[n1 + 64 n2], the twiddled results are
+// transposed through LDS, lane (k2, j) runs the DFT64 over n1; every load and
+// store is 512 contiguous bytes per wave.  Elements x with spec column
+// (x + L/2) mod L outside the live band are zero and not read.
+constexpr int NTR = 512;
+__global__ void __launch_bounds__(NTR) k_crop4k_rows(DevState st, float2 *out, const float2 *__restrict__ tw,
+                                                      float scale) {
+    __shared__ float2 lds[64 * 8 * 9];
+    const int i64 = threadIdx.x & 63, j = threadIdx.x >> 6;
+    float2 *row = out + ((size_t)blockIdx.y * L + blockIdx.x) * L;
+    float2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int x = i64 + 64 * (j + 8 * q), sx = (x + L / 2) & (L - 1);
+        v[q] = sx >= st.sx0 && sx <= st.sx1 ? row[x] : make_float2(0.f, 0.f);
+    }
+    idft64(v, lds, i64, j, tw);  // lane (n1 = i64, j): bracket values for k2 = j + 8 q
+    __syncthreads();             // the exchange reads are done: lds is the transpose tile now
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int k2 = j + 8 * q;
+        lds[i64 * 65 + k2] = cmul(v[q], cconj(tw[(i64 * k2) & (L - 1)]));  // A[n1][k2] W^{n1 k2}
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = lds[(j + 8 * q) * 65 + i64];  // lane (k2 = i64, j): A[j + 8 q][k2]
+    __syncthreads();             // before idft64's exchange overwrites lds
+    idft64(v, lds, i64, j, tw);  // X[k2 + 64 (j + 8 q)]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) row[i64 + 64 * (j + 8 * q)] = cscale(v[q], scale);
+}
 }  // namespace c4k
 
-static hipError_t launch_crop4096(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
-                                  hipStream_t s) {
+static hipError_t launch_crop4096(const DevState &st, float2 *out, const float2 *tw_L, hipStream_t s) {
     using namespace c4k;
     const dim3 grid(L / CW, 64, st.B);
     hipLaunchKernelGGL(k_crop4k_cols1, grid, dim3(NT), 0, s, st, out, tw_L);
     hipLaunchKernelGGL(k_crop4k_cols2, grid, dim3(NT), 0, s, out, tw_L);
-    // rows in place, scaled by 1/L^2; columns x with spec column (x + L/2) mod L
-    // outside the live band are zero
-    FftBand rows;
-    rows.elo = st.sx0;
-    rows.ehi = st.sx1;
-    rows.eroll = L / 2;
-    const size_t bs = (size_t)L * L;
-    return launch_fft_batch(true, out, out, pl_L, tw_L, L, st.B, bs, L, 1, bs, L, 1, 0, 0,
-                            1.0f / ((float)L * (float)L), s, nullptr, 1.f, rows);
+    hipLaunchKernelGGL(k_crop4k_rows, dim3(L, st.B), dim3(NTR), 0, s, st, out, tw_L, 1.0f / ((float)L * (float)L));
+    return hipGetLastError();
 }
 
 hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, const float2 *tw_L,
@@ -1047,7 +1073,7 @@ hipError_t launch_objcrop(const DevState &st, float2 *out, const FftPlan &pl_L, 
         const hipError_t r = launch_objcrop_regs(st, out, tw_L, s);
         if (r != hipErrorNotSupported) return r;
     }
-    if (st.L == c4k::L && !std::getenv("FPM_NO_CROP4K")) return launch_crop4096(st, out, pl_L, tw_L, s);
+    if (st.L == c4k::L && !std::getenv("FPM_NO_CROP4K")) return launch_crop4096(st, out, tw_L, s);
     const int L = st.L;
     const size_t bs = (size_t)L * L;
     // rows: spec rows (sequences) and columns (elements) outside the live band
