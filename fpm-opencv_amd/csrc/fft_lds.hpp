@@ -321,10 +321,25 @@ __device__ __forceinline__ float2 *stockham_t_ld(const LD &ld, float2 *a, float2
 }
 
 // ---- block reductions -------------------------------------------------------
+// Max over the 64 lanes, in every lane; the wave must be fully active.  DPP
+// moves within each row of 16 (xor 1 and 2 as quad permutes, then the
+// half-row and row mirrors), then the four row maxima by v_readlane: four VALU
+// moves instead of six ds_bpermute round trips through the LDS crossbar (the
+// __shfl_xor form).  max is exact, so the result is the same in any order.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
+    v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
+    v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror: the other quad of the 8
+    v = fmaxf(v, dpp_f<0x140>(v));  // row_mirror: the other 8 of the row
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 
 // Max over the block; `red` is LDS scratch of >= nwaves floats. Result valid

@@ -959,8 +959,8 @@ hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw
 // 3x the pass's bytes, 3.6 ms per iteration at config 5).  Here the column
 // IDFT runs first, straight from the (read-only) spectrum, as a six-step
 // 4096 = 64 x 64 transform whose passes read and write 128-byte row segments
-// of 16 adjacent columns; the row IDFT then runs in place on the contiguous
-// rows (the batched transform, element band = the live columns).  With
+// of 16 adjacent columns; the row IDFT then runs in place, the same 64 x 64
+// split inside a block per row (k_crop4k_rows).  With
 // n = n1 + 64 n2 and k = k2 + 64 k1 (inverse, W = e^{+2 pi i / 4096}):
 //   X[k2 + 64 k1] = sum_n1 W64^{n1 k1} [ W^{n1 k2} sum_n2 x[n1 + 64 n2] W64^{n2 k2} ]
 //   pass 1 (block n1): the bracket for all k2, stored at row k2 + 64 n1
