@@ -330,6 +330,17 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+// Sum over each row of 16 lanes, in every lane of the row, with exactly the
+// association of the xor butterfly o = 8, 4, 2, 1 (after the first step the
+// row is 8-periodic, so row_ror:4 reads the value lane ^ 4 holds, and so on):
+// bit-identical to the __shfl_xor form.  Each row must be fully active.
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0x128>(v);  // row_ror:8
+    v += dpp_f<0x124>(v);  // row_ror:4
+    v += dpp_f<0x122>(v);  // row_ror:2
+    v += dpp_f<0x121>(v);  // row_ror:1
+    return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
     v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2

@@ -500,11 +500,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                     if (m < TH / 16 - 1) wk = pmul(wk, wstep);
                 }
                 float2 s2 = pout(s2p);
-#pragma unroll
-                for (int o = 8; o > 0; o >>= 1) {
-                    s2.x += __shfl_xor(s2.x, o, 64);
-                    s2.y += __shfl_xor(s2.y, o, 64);
-                }
+                s2.x = row16_sum(s2.x);  // the group's 16 lanes (DPP, bit-identical to the xor butterfly)
+                s2.y = row16_sum(s2.y);
                 if (t == 0) tailF[pp] = h != hb ? cadd(tailF[pp], s2) : s2;
             }
             __syncthreads();  // half-T reusable; tailF

@@ -432,11 +432,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 if (m < 15) wk = pmul(wk, wstep);
             }
             float2 s2 = pout(s2p);
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) {
-                s2.x += __shfl_xor(s2.x, o, 64);
-                s2.y += __shfl_xor(s2.y, o, 64);
-            }
+            s2.x = row16_sum(s2.x);  // the group's 16 lanes (DPP, bit-identical to the xor butterfly)
+            s2.y = row16_sum(s2.y);
             if (t == 0) tailF[pp] = s2;
         }
         __syncthreads();  // tailF

@@ -58,8 +58,8 @@ static_assert(4 * 8 * CXP <= WTILE, "cross-group tile");
 
 // R1 holds its row's loads in registers (hoisted ahead of the pupil stores):
 // 128 VGPRs = 4 waves per SIMD with a few spills (measured 38.5 -> 36.3 us per
-// launch at config 5; 3 waves without the spills measured slower).  The same
-// hoisting in R2 measured slower (36.4 -> 40.0 us) and is not used.
+// launch at config 5; 3 waves without the spills measured slower).  R2 hoists
+// half a row at a time (all of it measured slower, 36.4 -> 40.0 us).
 
 namespace {
 
@@ -340,15 +340,28 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
     float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;
+    // the loads of half the row's pixels ahead of their stores (the stores may
+    // alias the loads, so the compiler keeps program order: one memory latency
+    // per pixel otherwise; config 5 +1.3 %, profiles/r04_ab/wave_dpp_r2_ab.txt;
+    // all sixteen ahead measured slower, 36.4 -> 40.0 us)
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int hp = 0; hp < 2; ++hp) {
+        float2 ov[8], pv[8];
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
+        for (int i = 0; i < 8; ++i) {
+            const int kx = fold(t + 16 * (4 * c + (i & 3)) + 256 * (2 * hp + (i >> 2)));
+            const bool in = kx * kx <= w2;
+            ov[i] = in ? spec_ld(st, b, srow + kx) : make_float2(0.f, 0.f);
+            pv[i] = in ? pup[kx] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int p = 2 * hp + (i >> 2), bb = i & 3;
             const int kx = fold(t + 16 * (4 * c + bb) + 256 * p);
             if (kx * kx > w2) continue;
             const size_t si = srow + kx;
-            const float2 o = spec_ld(st, b, si);                 // pre-update Objfcrop (:361)
-            const float2 pp = pup[kx];
+            const float2 o = ov[i];                              // pre-update Objfcrop (:361)
+            const float2 pp = pv[i];
             const float2 D = csub(x[4 * p + bb], cmul(o, pp));   // Objfup - ObjfcropP (:409,463)
             const float pa = cmag(pp);                           // object update (:406-419,433)
             const float2 dpc = cmul(cmul(D, cscale(cconj(pp), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
@@ -356,6 +369,7 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
             const float oa = cmag(o);                            // pupil numerator (:459-464,469)
             dP[kx] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
         }
+    }
 }
 
 }  // namespace
