@@ -130,42 +130,54 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
 
 // ---- K4 ---------------------------------------------------------------------
 // grid (ROI tile rows, B), block 256 or 1024: one tile row of the ROI box per block.
-// Each wave refreshes whole 16x16 tiles (4 pixels per lane, no barrier); the
-// block then folds the row's other (unchanged) tile maxima into rmax.
+// Each wave refreshes whole 16x16 tiles (4 pixels per lane, no barrier),
+// issuing every load of its tiles before the first reduction; the row's other
+// (unchanged) tile maxima are loaded first and folded in with one block max.
 // Block size: one wave per ROI tile column up to 16 waves (1024 threads for
 // config 5's 42-tile rows; 256 for config 3's 4-5 tiles, where 16 mostly
 // idle waves per block only added latency).
 template <int kRowThreads>
 __global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs sa) {
-    __shared__ float red[kRowThreads / 64];
-    extern __shared__ float fresh[];  // the ROI's tiles of this row
+    constexpr int NW = kRowThreads / 64, MT = 5;  // tiles a wave refreshes at once
+    __shared__ float red[NW];
     const int r = st.r, L = st.L, ntx = st.ntx;
     const int b = blockIdx.y;
     const int ty = (sa.yc - r) / kTile + blockIdx.x;
     const int tx0 = (sa.xc - r) / kTile, tx1 = (sa.xc + r) / kTile;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float *tmax = st.tmax + (size_t)b * st.nty * ntx + (size_t)ty * ntx;
-    for (int tx = tx0 + w; tx <= tx1; tx += kRowThreads / 64) {
-        float m = 0.f;
+    // the row's unchanged tile maxima first: their loads overlap the refresh
+    float mx = 0.f;
+    for (int tx = threadIdx.x; tx < ntx; tx += kRowThreads)
+        if (tx < tx0 || tx > tx1) mx = fmaxf(mx, tmax[tx]);
+    // the ROI tiles: every load of a wave's (up to MT) tiles before the first
+    // reduction -- one memory latency instead of one per tile
+    for (int base = tx0 + w; base <= tx1; base += MT * NW) {
+        float m[MT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int p = lane + 64 * j;
-            const int y = ty * kTile + (p >> 4), x = tx * kTile + (p & 15);
-            if (y < L && x < L) m = fmaxf(m, cmag(spec_ld(st, b, (size_t)y * L + x)));
+        for (int i = 0; i < MT; ++i) {
+            const int tx = base + i * NW;
+            m[i] = 0.f;
+            if (tx <= tx1) {  // wave-uniform
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int p = lane + 64 * j;
+                    const int y = ty * kTile + (p >> 4), x = tx * kTile + (p & 15);
+                    if (y < L && x < L) m[i] = fmaxf(m[i], cmag(spec_ld(st, b, (size_t)y * L + x)));
+                }
+            }
         }
-        m = wave_max(m);
-        if (lane == 0) {
-            tmax[tx] = m;
-            fresh[tx - tx0] = m;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int tx = base + i * NW;
+            if (tx > tx1) break;  // wave-uniform
+            const float t = wave_max(m[i]);
+            if (lane == 0) tmax[tx] = t;
+            mx = fmaxf(mx, t);
         }
     }
-    __syncthreads();
-    // the refreshed tiles come from LDS, the rest of the row is unchanged
-    float m = 0.f;
-    for (int tx = threadIdx.x; tx < ntx; tx += kRowThreads)
-        m = fmaxf(m, (tx >= tx0 && tx <= tx1) ? fresh[tx - tx0] : tmax[tx]);
-    m = block_max(m, red);
-    if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = m;
+    mx = block_max(mx, red);
+    if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = mx;
 }
 
 // ---- K5 ---------------------------------------------------------------------
@@ -875,9 +887,9 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     const int nrow = (sa.yc + st.r) / kTile - (sa.yc - st.r) / kTile + 1;
     const int ncol = (sa.xc + st.r) / kTile - (sa.xc - st.r) / kTile + 1;
     if (ncol > 8)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<1024>), dim3(nrow, st.B), dim3(1024), ncol * sizeof(float), s, st, sa);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<1024>), dim3(nrow, st.B), dim3(1024), 0, s, st, sa);
     else
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<256>), dim3(nrow, st.B), dim3(256), ncol * sizeof(float), s, st, sa);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<256>), dim3(nrow, st.B), dim3(256), 0, s, st, sa);
     // Np 1024: the commit is folded into the next LED's row IDFT (np1024.hip)
     // and runs here only after the iteration's last LED (launch_pupil_commit)
     if (!(st.np == 1024 && st.meas_g == 1024))
