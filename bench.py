@@ -525,13 +525,19 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "LED-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+            # the no-flag default changed in round 4 (weak, 256 patches per rank in rounds 1-3 -> strong,
+            # one 256-patch field): multi-GPU lines of r01-r03 and r04+ are not comparable
+            "scaling_note": "default since round 4: strong scaling of north_star's 256-patch field; "
+                            "rounds 1-3 defaulted to weak scaling (256 patches per rank); --weak reproduces that",
             "dtype": "f32 (fp16 spectrum storage)" if fp16 else "f32",
             "data": ("synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16"
                      if args.data == "model" else "random uint16 (profiling only)"),
             "config": {"workload": WORKLOADS[args.config] if args.np == 256 or args.config != "metric" else
                                    f"dogStomach optics, Np={geo['np_']}, one runFPM iteration per step",
                        "patches_per_gpu": B, "leds": int(geo["n_led"]), "np": int(geo["np_"]),
-                       **({"patches_total": args.patches_total} if strong else {}),
+                       "patches_total": int(args.patches_total if strong else B * world),
+                       "scaling_mode": (f"strong: one {args.patches_total}-patch field sharded over {world} rank(s)"
+                                        if strong else f"weak: {B} patches per rank"),
                        "nlarge": int(geo["L"]), "na_radius": int(geo["r"]),
                        "path": "fused" if info.path == fpm_amd.PATH_FUSED else "general",
                        "kernel": kernel_name(info), "workgroups_per_patch": int(info.wg_per_patch),

@@ -14,6 +14,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <algorithm>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -74,6 +75,41 @@ hipError_t launch_preprocess_frame(const uint16_t *frame, int width, int np, int
                                    double dark_mult, bool darkfield, unsigned long long *sums, uint16_t *out,
                                    int16_t *bg_out_dev, hipStream_t s);
 size_t fused_T_elems(int np, int r, int B);
+
+// Co-resident grids (split / distributed modes, fused_sync.hpp): the
+// occupancy check, then a plain launch ordered after the previous co-resident
+// grid of this process on the same device (another context, another stream),
+// so two grids that each need every block resident never share the device.
+// Under stream capture the order is the capturing caller's business (an event
+// recorded outside the capture cannot be waited on inside it).
+hipError_t launch_coresident_raw(const void *fn, int grid, int block, size_t lds, void **args, hipStream_t s) {
+    int dev = 0, n_cu = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
+    if (e != hipSuccess) return e;
+    if ((long long)per_cu * n_cu < grid) return hipErrorCooperativeLaunchTooLarge;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if ((e = hipStreamIsCapturing(s, &cap)) != hipSuccess) return e;
+    if (cap != hipStreamCaptureStatusNone) return hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s);
+    constexpr int kMaxDev = 64;
+    struct Serial {
+        std::mutex mu;
+        hipEvent_t last = nullptr;  // completion of the device's latest co-resident grid
+    };
+    static Serial serial[kMaxDev];
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    Serial &sd = serial[dev];
+    std::lock_guard<std::mutex> lk(sd.mu);
+    if (!sd.last && (e = hipEventCreateWithFlags(&sd.last, hipEventDisableTiming)) != hipSuccess) {
+        sd.last = nullptr;
+        return e;
+    }
+    // an event never recorded counts as complete, so the first wait is free
+    if ((e = hipStreamWaitEvent(s, sd.last, 0)) != hipSuccess) return e;
+    if ((e = hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s)) != hipSuccess) return e;
+    return hipEventRecord(sd.last, s);
+}
 }  // namespace fpm
 
 using namespace fpm;
@@ -860,19 +896,9 @@ int fpm_download_objcrop_device(fpm_ctx *c, float *dst) {
 
 int fpm_abi_version(void) { return FPM_ABI_VERSION; }
 
-int fpm_get_info_sized(const fpm_ctx *c, fpm_info *info, size_t info_size) {
-    if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
-    if (info_size < offsetof(fpm_info, fused_kernel))
-        return set_err(FPM_ERR_INVAL, "fpm_info of %zu bytes predates every released layout", info_size);
-    fpm_info full;
-    const int rc = fpm_get_info(c, &full);
-    if (rc) return rc;
-    std::memcpy(info, &full, std::min(info_size, sizeof full));
-    return FPM_OK;
-}
-
-int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
-    if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
+// The whole fpm_info of this header (every field of every ABI revision).
+static void fill_info(const fpm_ctx *c, fpm_info *info) {
+    std::memset(info, 0, sizeof *info);
     info->path = c->path;
     info->box = c->st.nb;
     info->support_px = c->support_px;
@@ -889,6 +915,27 @@ int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
                            : c->fused_s90 || c->fused_small ? 1024
                            : c->fused_mr ? 768
                                          : c->fused_nt;
+}
+
+int fpm_get_info_sized(const fpm_ctx *c, fpm_info *info, size_t info_size) {
+    if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
+    if (info_size < FPM_INFO_V3_SIZE)
+        return set_err(FPM_ERR_INVAL, "fpm_info of %zu bytes predates every released layout", info_size);
+    fpm_info full;
+    fill_info(c, &full);
+    std::memcpy(info, &full, std::min(info_size, sizeof full));
+    return FPM_OK;
+}
+
+// Frozen at the ABI-3 layout (FPM_INFO_V3_SIZE bytes, the fields up to
+// fused_kernel): a binary built against that header passes a struct of that
+// size, so this entry point never writes past it.  Later fields are reported
+// through fpm_get_info_sized only.
+int fpm_get_info(const fpm_ctx *c, fpm_info *info) {
+    if (!c || !info) return set_err(FPM_ERR_INVAL, "null argument");
+    fpm_info full;
+    fill_info(c, &full);
+    std::memcpy(info, &full, FPM_INFO_V3_SIZE);
     return FPM_OK;
 }
 

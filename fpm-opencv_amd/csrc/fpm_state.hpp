@@ -128,6 +128,10 @@ __device__ __forceinline__ float h16_scale(float m, float *inv) {
     int e = 0;
     (void)frexpf(m, &e);  // m < 2^e
     if (!(m > 0.f)) e = 0;
+    // a block maximum below 2^-100 keeps the scale 2^114 (finite): an
+    // unclamped 2^(14 - e) overflows to +inf for e < -113 and turns the
+    // block's exact zeros into NaN (0 * inf)
+    if (e < -100) e = -100;
     *inv = ldexpf(1.0f, e - 14);
     return ldexpf(1.0f, 14 - e);
 }

@@ -15,8 +15,9 @@ namespace fpm {
 // invalidate the whole XCD L2 that the other patches' streams use.)
 //   publish: every wave waits for its own stores to be acknowledged, then one
 //            thread stores the flag.
-//   wait:    one thread polls the flag (s_sleep between polls) and gives up
-//            after ~1 s, raising abort_flag so the partner leaves too.
+//   wait:    lane p of the first wave polls part p's flag (one vector load
+//            per spin, s_sleep between spins) and gives up after ~1 s,
+//            raising abort_flag so the partners leave too.
 // Co-located parts (every workgroup reports the same XCC_ID): the XCD's L2
 // is the coherence point, so stores stay plain (the L1 writes through and the
 // line stays in that L2) and loads bypass the L1 with the sc1 policy: L2
@@ -102,19 +103,21 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
 // distributed modes): every block must be resident at once.  The grid is
 // checked against the occupancy query -- the check hipLaunchCooperativeKernel
 // makes -- and launched plainly: the same residency (MI355X_MICROARCH.md
-// "coop-launch") without the cooperative launch's per-launch host cost.  Every
-// wait in those kernels also gives up after ~1 s and raises the sticky abort
-// word, so a grid that could not be co-resident fails instead of hanging.
+// "coop-launch") without the cooperative launch's per-launch host cost.
+// Two such grids must never run side by side on one device (each could get
+// only part of its blocks resident and both would wait for the rest), so
+// launch_coresident_raw (api.cpp) orders every co-resident grid of the
+// process on a device after the previous one: a per-device mutex, a wait on
+// the previous grid's completion event, a new event after the launch -- what
+// the cooperative launch's serialisation gave.  Across processes a device is
+// single-tenant for these modes.  Every wait in those
+// kernels also gives up after ~1 s and raises the sticky abort word, so a grid
+// that could not be co-resident fails instead of hanging.
+hipError_t launch_coresident_raw(const void *fn, int grid, int block, size_t lds, void **args, hipStream_t s);
 template <class Args>
 inline hipError_t launch_coresident(const void *fn, int grid, int block, size_t lds, Args *a, hipStream_t s) {
-    int dev = 0, n_cu = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds);
-    if (e != hipSuccess) return e;
-    if ((long long)per_cu * n_cu < grid) return hipErrorCooperativeLaunchTooLarge;
     void *args[] = {a};
-    return hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s);
+    return launch_coresident_raw(fn, grid, block, lds, args, s);
 }
 
 }  // namespace fpm

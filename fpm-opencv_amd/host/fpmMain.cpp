@@ -311,7 +311,7 @@ int main(int argc, char **argv) {
         return 1;
     }
     fpm_info info;
-    fpm_get_info(ctx, &info);
+    fpm_get_info_sized(ctx, &info, sizeof info);
     fpm_destroy(ctx);
     fpm_host_close(h);
     bool ok;

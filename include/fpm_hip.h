@@ -29,9 +29,9 @@
 extern "C" {
 #endif
 
-/* ABI revision of this header.  Round 4 (4): fpm_info gained threads_per_wg;
- * fpm_get_info_sized lets a caller built against an older header pass its
- * smaller struct.  fpm_abi_version() reports the library's revision. */
+/* ABI revision of this header.  Round 4 (4): fpm_info gained threads_per_wg,
+ * readable only through fpm_get_info_sized (fpm_get_info keeps writing the
+ * ABI-3 struct size).  fpm_abi_version() reports the library's revision. */
 #define FPM_ABI_VERSION   4
 
 #define FPM_OK            0
@@ -143,6 +143,9 @@ typedef struct fpm_info {
     int32_t threads_per_wg;/* threads per workgroup of the LED-update kernel (ABI 4) */
 } fpm_info;
 
+/* bytes of the ABI-3 struct, fields path .. fused_kernel: what fpm_get_info writes */
+#define FPM_INFO_V3_SIZE  (offsetof(fpm_info, fused_kernel) + sizeof(int32_t))
+
 /* Per-kernel timing of the most recent fpm_run, from HIP events recorded on
  * the stream the kernels were launched on. */
 typedef struct fpm_timing {
@@ -200,9 +203,12 @@ int  fpm_download_objcrop_device(fpm_ctx *ctx, float *dst_dev);
 /* Use a caller-provided hipStream_t (NULL = the context's own stream). */
 int  fpm_set_stream(fpm_ctx *ctx, void *hip_stream);
 
-/* fpm_get_info fills the fpm_info of THIS header; fpm_get_info_sized writes
- * only the first info_size bytes (pass sizeof(fpm_info) of the header the
- * caller was built with: fields are only ever appended). */
+/* fpm_get_info is frozen at the ABI-3 layout: it writes FPM_INFO_V3_SIZE
+ * bytes (path .. fused_kernel) and never a later field, so a binary built
+ * against the ABI-3 header, whose struct is that size, stays safe.  Fields
+ * appended since (threads_per_wg, ABI 4) are read with fpm_get_info_sized,
+ * which writes only the first info_size bytes: pass sizeof(fpm_info) of the
+ * header the caller was built with (fields are only ever appended). */
 int  fpm_get_info(const fpm_ctx *ctx, fpm_info *info);
 int  fpm_get_info_sized(const fpm_ctx *ctx, fpm_info *info, size_t info_size);
 int  fpm_get_timing(const fpm_ctx *ctx, fpm_timing *timing);

@@ -65,6 +65,46 @@ def test_bench_kernel_256_patches_vs_oracle():
             assert e < 1e-5, (k, b, e)
 
 
+@pytest.mark.parametrize("B,ks", [(64, 4), (32, 8)], ids=["shard64_dist4", "shard32_dist8"])
+def test_strong_scaling_shard_vs_oracle(B, ks):
+    """The instances behind north_star's 4- and 8-GPU points at their real
+    size: a 64- / 32-patch shard of the metric geometry, no env override, so
+    the context auto-selects k_fused_dist<4> / <8> exactly as bench.py does
+    (256 co-resident workgroups: full occupancy, XCD placement of the parts
+    and the local / remote handoff mix of the bench run).  One iteration;
+    first / middle / last patch vs the oracle (fpmMain.cpp:345-476)."""
+    import torch
+    import oracle_lib
+    from tools.synth_torch import make_stack
+    geo = _metric()
+    order = np.arange(geo["n_led"])
+    for k in ("FPM_DIST", "FPM_SPLIT", "FPM_NO_DIST", "FPM_NO_SPLIT"):
+        assert k not in os.environ, k
+    stack = make_stack(geo["np_"], geo["L"], geo["r"], geo["x0"], geo["y0"], B, seed=20261015 + B, device="cuda")
+    prob = fpm_amd.Problem(geo["np_"], geo["L"], order, geo["x0"], geo["y0"], geo["r"], geo["d1"], geo["d2"],
+                           n_patch=B)
+    with fpm_amd.Solver(prob) as s:
+        info = s.info()
+        assert info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256_DIST and info.wg_per_patch == ks, \
+            (info.fused_kernel, info.wg_per_patch)
+        assert ks * B == 256  # every CU holds one part
+        torch.cuda.synchronize()
+        s.upload_device(stack.data_ptr())
+        s.init()
+        s.run(1)
+        out = s.download(objF=False, support=False)
+    sample = (0, B // 2, B - 1)
+    host = stack[:, list(sample)].cpu().numpy().view(np.uint16)
+    del stack
+    refs = oracle_lib.run_fpm_batch(host, order, geo["x0"], geo["y0"], geo["np_"], geo["L"], geo["r"], geo["d1"],
+                                    geo["d2"], 1, threads=3, pupil=True)
+    for i, b in enumerate(sample):
+        for k in ("objCrop", "pupil"):
+            e = rel_l2(out[k][b], refs[k][i])
+            print(f"{B}-patch shard, k_fused_dist<{ks}>, patch {b}, {k}: rel L2 {e:.2e}")
+            assert e < 1e-5, (k, b, e)
+
+
 @pytest.mark.parametrize("ks,dist", [(2, False), (4, False), (4, True), (8, True)],
                          ids=["split2", "split4", "dist4", "dist8"])
 def test_metric_geometry_5_iterations_vs_oracle(ks, dist):
