@@ -12,11 +12,14 @@ import tempfile
 
 import numpy as np
 
-CASES = [  # (name, environment): Np 256 metric-like geometry, r 33 (tail rows and tail pixels)
-    ("one_workgroup", {"FPM_NO_DIST": "1", "FPM_NO_SPLIT": "1"}),
-    ("split_ks2", {"FPM_NO_DIST": "1", "FPM_SPLIT": "2"}),
-    ("dist_ks4", {"FPM_DIST": "4"}),
-    ("dist_ks8", {"FPM_DIST": "8"}),
+G256 = (256, 768, 33, 3, 60)  # Np, L, r, LED grid side, step: metric-like, tail rows and tail pixels
+CASES = [  # (name, environment, geometry)
+    ("one_workgroup", {"FPM_NO_DIST": "1", "FPM_NO_SPLIT": "1"}, G256),
+    ("split_ks2", {"FPM_NO_DIST": "1", "FPM_SPLIT": "2"}, G256),
+    ("dist_ks4", {"FPM_DIST": "4"}, G256),
+    ("dist_ks8", {"FPM_DIST": "8"}, G256),
+    ("np90_s90", {}, (90, 360, 30, 5, 24)),       # k_fused_s90 (configs 1 / 2)
+    ("np200_mr", {}, (200, 600, 26, 5, 40)),      # k_fused_mr (config 3)
 ]
 
 CHILD = r"""
@@ -24,8 +27,8 @@ import sys, numpy as np
 sys.path.insert(0, 'fpm-opencv_amd/python'); sys.path.insert(0, '.')
 import fpm_amd
 from tools.synth import grid_geometry, make_stack
-Np, L, r = 256, 768, 33
-x0, y0, order = grid_geometry(Np, L, 3, 60)
+Np, L, r, nside, step = (int(v) for v in sys.argv[2:7])
+x0, y0, order = grid_geometry(Np, L, nside, step)
 stack = make_stack(Np, L, r, x0, y0, n_patch=4, seed=7)
 prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=4)
 out = fpm_amd.run_fpm(prob, stack, 2)
@@ -33,19 +36,19 @@ np.savez(sys.argv[1], **{k: np.asarray(out[k]) for k in ("objF", "objCrop", "pup
 """
 
 
-def run(lib, env, path):
+def run(lib, env, geo, path):
     e = dict(os.environ, FPM_HIP_LIB=os.path.abspath(lib), **env)
-    subprocess.run([sys.executable, "-c", CHILD, path], check=True, env=e, timeout=300)
+    subprocess.run([sys.executable, "-c", CHILD, path, *map(str, geo)], check=True, env=e, timeout=300)
 
 
 def main():
     a, b = sys.argv[1], sys.argv[2]
     ok = True
     with tempfile.TemporaryDirectory() as d:
-        for name, env in CASES:
+        for name, env, geo in CASES:
             pa, pb = os.path.join(d, f"{name}_a.npz"), os.path.join(d, f"{name}_b.npz")
-            run(a, env, pa)
-            run(b, env, pb)
+            run(a, env, geo, pa)
+            run(b, env, geo, pb)
             za, zb = np.load(pa), np.load(pb)
             same = all(np.array_equal(za[k], zb[k]) for k in za.files)
             ok = ok and same
