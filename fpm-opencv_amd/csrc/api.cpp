@@ -805,7 +805,7 @@ int fpm_run(fpm_ctx *c, int iters) {
                                         "P",      "A:rowIDFT",   "C:rowDFT",  "upd:body",    "B:loop",
                                         "split:Fstores", "split:Fwait"};
         const char *names_d[kStamps] = {"gather", "A", "sync1", "B", "sync2", "C", "update", "sync3",
-                                        "merge+Opre", "max", "P", "-", "-"};
+                                        "merge+Opre", "max", "P", "C:rows(sub)", "sync3:acks(sub)"};
         const char *const *names = c->dist ? names_d : names_f;
         for (int v = 0; v < 2; ++v) {
             fprintf(stderr, "[fpm stamps] cycles per LED step (%s wave view, mean over blocks):", v ? "last" : "first");

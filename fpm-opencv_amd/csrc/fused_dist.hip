@@ -415,6 +415,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) v[m] = ron ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
             dft256_out6(v, F, scr, wt, t, xrd);
+#ifdef FPM_DIST_SUBSTAMP
+            FPM_STAMP(11)  // C: own FFT rows (waves with rows)
+#endif
         } else {
 #pragma unroll
             for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
@@ -485,6 +488,10 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 make_float2(tmx[bk], __uint_as_float((dirty[bk >> 5] >> (bk & 31)) & 1u)));
         }
         FPM_STAMP(6)
+#ifdef FPM_DIST_SUBSTAMP
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's spectrum / tile stores acknowledged
+        FPM_STAMP(12)
+#endif
         if (!handoff()) {  // ---- sync 3
             aborted = true;
             break;

@@ -17,7 +17,7 @@ timeout -k 10 600 python tools/gpu/cmp_libs.py fpm-opencv_amd/lib/libfpm_hip.so 
 fi
 args() { case $1 in metric) echo "";; pt128) echo "--patches-total 128";; pt64) echo "--patches-total 64";; pt32) echo "--patches-total 32";; c2) echo "--config c2";; c3) echo "--config c3";; c5) echo "--config c5";; esac; }
 for w in ${STAMPS:-}; do
-  for V in new $BASE; do
+  for V in ${STLIBS:-new $BASE}; do
     if [ $V = new ]; then unset FPM_HIP_LIB; else export FPM_HIP_LIB=$GRAFT_REPO_ROOT/fpm-opencv_amd/lib_$V/libfpm_hip.so; fi
     FPM_STAMPS=1 timeout -k 10 120 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-gather $(args $w) > $O/st_${w}_$V.json 2> $O/st_${w}_$V.err || { echo "stamps $w $V rc=$?"; tail -3 $O/st_${w}_$V.err; exit 1; }
     echo "== stamps $w $V"; grep "fpm stamps" $O/st_${w}_$V.err | tail -2
