@@ -196,21 +196,6 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
         for (int s = 0; s < 6; ++s) Opre[s] = ldO(sr, s);
     }
-#ifdef FPM_MR_EARLY_I
-    // the measurement of each wave's first pass-B column block of the NEXT
-    // LED, loaded with its spectrum window after the update barrier
-    uint2 mpre[5];
-    auto load_mpre = [&](int itn) {
-        const int x = GPW * w + gw;
-        if (act && x < NP) {
-            const uint16_t *Ibn = a.meas + ((size_t)a.order[itn] * st.B + b) * NP * NP;
-            const uint2 *ip = (const uint2 *)(Ibn + (x * N2 + l) * N1);
-#pragma unroll
-            for (int i = 0; i < 5; ++i) mpre[i] = ip[i];
-        }
-    };
-    if (a.n_order > 0) load_mpre(0);
-#endif
     for (int it = 0; it < a.n_order; ++it) {
         const int led = a.order[it];
         const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
@@ -252,18 +237,10 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             nx = __builtin_amdgcn_readfirstlane(nx);
             const int x = GPW * cb + gw;
             if (act && x < NP) {
+            const uint2 *ip = (const uint2 *)(Ib + (x * N2 + l) * N1);  // 20 uint16, 8-B aligned
             uint2 mi[5];
-#ifdef FPM_MR_EARLY_I
-            if (cb == w) {  // the wave's first block: loaded after the previous update barrier
 #pragma unroll
-                for (int i = 0; i < 5; ++i) mi[i] = mpre[i];
-            } else
-#endif
-            {
-                const uint2 *ip = (const uint2 *)(Ib + (x * N2 + l) * N1);  // 20 uint16, 8-B aligned
-#pragma unroll
-                for (int i = 0; i < 5; ++i) mi[i] = ip[i];
-            }
+            for (int i = 0; i < 5; ++i) mi[i] = ip[i];
 #pragma unroll
             for (int k = 0; k < 20; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
@@ -338,9 +315,6 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             const float2 *sr = window(it + 1);
 #pragma unroll
             for (int s = 0; s < 6; ++s) Opre[s] = ldO(sr, s);
-#ifdef FPM_MR_EARLY_I
-            load_mpre(it + 1);
-#endif
         }
         FPM_STAMP(4)
 

@@ -159,21 +159,6 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         return ((inmask >> k) & 1) ? sr[kyr * L + f90_fold(l + 10 * k)] : make_float2(0.f, 0.f);
     };
     float2 Opre[9];
-#ifdef FPM_S90_EARLY_I
-    // this column's measurement run of the NEXT LED, loaded with its spectrum
-    // window right after the update barrier (its latency under max, pupil
-    // and pass A)
-    uint32_t mi[5] = {0u, 0u, 0u, 0u, 0u};
-    auto load_mi = [&](int itn) {
-        if (con && l < 9) {
-            const uint16_t *Ibn = a.meas + ((size_t)a.order[itn] * st.B + b) * NP * NP;
-            const uint32_t *ip = (const uint32_t *)(Ibn + (g * 9 + l) * 10);  // 20 B, 4-B aligned
-#pragma unroll
-            for (int i = 0; i < 5; ++i) mi[i] = ip[i];
-        }
-    };
-    if (a.n_order > 0) load_mi(0);
-#endif
     if (a.n_order > 0) {
         const float2 *sr = window(0);
 #pragma unroll
@@ -216,16 +201,12 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         }
         // this column's measurement run, issued before the barrier (its
         // latency overlaps the wait): lane j < 9 holds I[j + 9 k][x], k < 10
-#ifndef FPM_S90_EARLY_I
         uint32_t mi[5] = {0u, 0u, 0u, 0u, 0u};
         if (con && l < 9) {
             const uint32_t *ip = (const uint32_t *)(Ib + (g * 9 + l) * 10);  // 20 B, 4-B aligned
 #pragma unroll
             for (int i = 0; i < 5; ++i) mi[i] = ip[i];
         }
-#else
-        (void)Ib;
-#endif
         __syncthreads();  // T complete; the previous LED's max|P| partials
         FPM_STAMP(7)
         if (it > 0) {  // max|P| of the previous pupil update (:415)
@@ -302,9 +283,6 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
             const float2 *sr = window(it + 1);
 #pragma unroll
             for (int k = 0; k < 9; ++k) Opre[k] = ldO(sr, k);
-#ifdef FPM_S90_EARLY_I
-            load_mi(it + 1);
-#endif
         }
         FPM_STAMP(4)
 
