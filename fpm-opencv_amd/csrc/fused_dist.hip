@@ -251,21 +251,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (towner) Ot = cld(rs, wbase(itn) + tp.x * L + tp.y);
     };
     if (a.n_order > 0) load_window(0);
-    // the measurement of each wave's FIRST pass-B column block of the NEXT LED
-    // is loaded right after the merge of this LED (its HBM latency then runs
-    // under the max, pupil, gather, pass A and sync 1 instead of inside pass
-    // B, where at KS 8 each wave has a single block and nothing else to
-    // overlap it with); later blocks (KS 4) load as before
-    constexpr int CBq = TH / 4 < 16 ? TH / 4 : 16;
-    const int xl0 = (w % CBq) + CBq * gg + 4 * CBq * (w / CBq);  // colx(w)
-    uint4 preI[2];
-    auto prefetch_I = [&](int itn) {
-        const uint16_t *Ibn = a.meas + ((size_t)a.order[itn] * st.B + b) * NP * NP;
-        const uint4 *ip = (const uint4 *)(Ibn + ((xl0 + TH * hown) * 16 + t) * 16);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) preI[i] = ld_stream(ip + i);
-    };
-    if (a.n_order > 0 && w < NBLK) prefetch_I(0);
     const float epsn = st.eps * (float)(NP * NP);
     const float epsn_im = st.eps_im * (float)(NP * NP);
     unsigned *tmu = (unsigned *)tmx;
@@ -379,12 +364,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                     int nx = 0;
                     if (lane == 0) nx = atomicAdd(ccnt, 1);
                     nx = __builtin_amdgcn_readfirstlane(nx);
-                    if (r8 == w) {  // the wave's first block: prefetched (wave-uniform)
-                        cI[0] = preI[0];
-                        cI[1] = preI[1];
-                    } else {
-                        ldI(xl, cI);
-                    }
+                    ldI(xl, cI);
 #pragma unroll
                     for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
@@ -534,7 +514,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             tmx[bk] = m;
             if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
         }
-        if (it + 1 < a.n_order && w < NBLK) prefetch_I(it + 1);
         __syncthreads();
         FPM_STAMP(8)
 
