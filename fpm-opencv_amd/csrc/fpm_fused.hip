@@ -42,7 +42,6 @@
 #include "fused256.hpp"
 #include "fused_common.hpp"
 #include "fused_sync.hpp"
-#include "tilemax.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -95,8 +94,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     float *tmx = (float *)(tky + MAXTAILROWS);      // nbt: max|spec| per band tile (upper bound if dirty)
     unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits: tile max may be stale-high
     int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // [0] pass-B column-block counter, [1] handoff result
-    float *rowc = (float *)(ccnt + 2);              // kMaxBandRows: clean maximum per band tile row
-    float *rowd = rowc + kMaxBandRows;              // kMaxBandRows: dirty bound per band tile row
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
@@ -171,9 +168,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             P[j][s] = in ? pup[(kyr[j] + R) * NB + kx + R] : make_float2(0.f, 0.f);
         }
     }
-    __syncthreads();  // tpx / tky / sig; tile maxima and dirty bits
-    const TileRows trow{tmx, dirty, rowc, rowd, a.nbx, a.nbt / a.nbx};
-    trow.rebuild(w, NW, lane);  // read after the next LED's first barrier
+    __syncthreads();  // tpx / tky / sig
     // per-lane half-T row offsets of this lane's six column slots; rows
     // outside the box read the zero row `nrows` and write the dummy row after it
     const int zoff = nrows * TLD;
@@ -638,21 +633,29 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         FPM_STAMP(4)
 
         // ---- exact max|objF| (:460,467): max over clean tiles; dirty tiles
-        // only matter (and are re-read) when their bound exceeds that max.
-        // Per-tile-row maxima (tilemax.hpp): every wave forms the band's
-        // maxima itself from the untouched rows' maxima and the window rows'
-        // tiles -- no barrier on this path
-        float cm, dm;
-        trow.band_max(((yc - R) >> 4) - a.bty0, ((yc + R) >> 4) - a.bty0, w, NW, lane, cm, dm);
-        float omax = cm;
-#ifdef FPM_MAX_SUBSTAMP
-        if constexpr (!split) {
-            FPM_STAMP(11)  // band maxima
-            if (a.dbg && dm > cm) acc[12] += 1000;  // rescans per 1000 LED steps
+        // only matter (and are re-read) when their bound exceeds that max
+        float cm = 0.f, dm = 0.f;
+        for (int k = tid; k < a.nbt; k += NT) {
+            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
+            if (d) dm = fmaxf(dm, tmx[k]);
+            else cm = fmaxf(cm, tmx[k]);
         }
-#endif
-        if (dm > cm) {  // uniform (every wave computed the same cm, dm): rare (bright-field LEDs)
-            __syncthreads();  // every wave's band_max reads are done
+        cm = wave_max(cm);
+        dm = wave_max(dm);
+        if (lane == 0) {
+            red[w] = cm;
+            red[16 + w] = dm;
+        }
+        __syncthreads();
+        cm = red[0];
+        dm = red[16];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            cm = fmaxf(cm, red[i]);
+            dm = fmaxf(dm, red[16 + i]);
+        }
+        float omax = cm;
+        if (dm > cm) {  // block-uniform: rare (bright-field LEDs, first LED of an iteration)
             for (int k = w; k < a.nbt; k += NW) {
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;  // wave-uniform
                 const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
@@ -669,9 +672,16 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 }
             }
             __syncthreads();
-            trow.rebuild(w, NW, lane);
+            float m2 = 0.f;
+            for (int k = tid; k < a.nbt; k += NT)
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
+            m2 = wave_max(m2);
+            __syncthreads();  // red[] reads above are done
+            if (lane == 0) red[w] = m2;
             __syncthreads();
-            omax = trow.clean_max(lane);  // the re-read tiles are clean; every dirty bound left is <= cm
+            omax = red[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
         }
         FPM_STAMP(5)
         const float rom = 1.0f / omax;
@@ -729,8 +739,7 @@ size_t fused_lds_bytes(int ks, int nbt, int n_tail_rows) {
     const int tld = part_cols(ks) + 1;
     return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * sizeof(int2) + fz::MAXTAILROWS * sizeof(int) +
-           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int) +
-           2 * kMaxBandRows * sizeof(float);
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
 
 }  // namespace
@@ -742,7 +751,6 @@ int fused_threads(int np, int r, int L, const DevState &st) {
     if (!g.ok || L % kTile != 0) return 0;
     if (st.sy0 < 0 || st.sy1 >= L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= L || st.sx0 > st.sx1) return 0;
     const Band bd = band_of(st);
-    if (bd.nbt / bd.nbx > kMaxBandRows) return 0;
     return fused_lds_bytes(1, bd.nbt, g.n_tail_rows) <= 160 * 1024 ? 512 : 0;
 }
 
@@ -810,7 +818,6 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.nbx = bd.nbx;
     a.nbt = bd.nbt;
     a.rnbx = 1.0f / (float)a.nbx;
-    if (a.nbt / a.nbx > kMaxBandRows) return hipErrorInvalidValue;
     a.dbg = dbg;
     a.xch = ks > 1 ? xch : nullptr;
     a.flags = ks > 1 ? flags : nullptr;

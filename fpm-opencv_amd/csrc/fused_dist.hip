@@ -43,7 +43,6 @@
 #include "fused256.hpp"
 #include "fused_common.hpp"
 #include "fused_sync.hpp"
-#include "tilemax.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -80,8 +79,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     float *tmx = (float *)(tpq + MAXTAIL);          // nbt: max|spec| per band tile (upper bound if dirty)
     unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits
     int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // [0] pass-B block counter, [1] handoff result
-    float *rowc = (float *)(ccnt + 2);              // kMaxBandRows: clean maximum per band tile row
-    float *rowd = rowc + kMaxBandRows;              // kMaxBandRows: dirty bound per band tile row
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
@@ -152,9 +149,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         inmask |= (in ? 1u : 0u) << s;
         P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
-    __syncthreads();  // tpx / tpq / sig; tile maxima and dirty bits
-    const TileRows trow{tmx, dirty, rowc, rowd, a.nbx, a.nbt / a.nbx};
-    trow.rebuild(w, NW, lane);  // read after the next LED's barriers
+    __syncthreads();  // tpx / tpq / sig
     const int zoff = nrows * TLD;
     int roff[6];
 #pragma unroll
@@ -517,13 +512,29 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         __syncthreads();
         FPM_STAMP(8)
 
-        // ---- exact max|objF| (:460,467), identical in every part: per-tile-row
-        // maxima (tilemax.hpp), every wave forms the band's maxima itself
-        float cm, dm;
-        trow.band_max(((yc - R) >> 4) - a.bty0, ((yc + R) >> 4) - a.bty0, w, NW, lane, cm, dm);
+        // ---- exact max|objF| (:460,467), identical in every part
+        float cm = 0.f, dm = 0.f;
+        for (int k = tid; k < a.nbt; k += NT) {
+            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
+            if (d) dm = fmaxf(dm, tmx[k]);
+            else cm = fmaxf(cm, tmx[k]);
+        }
+        cm = wave_max(cm);
+        dm = wave_max(dm);
+        if (lane == 0) {
+            red[w] = cm;
+            red[16 + w] = dm;
+        }
+        __syncthreads();
+        cm = red[0];
+        dm = red[16];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            cm = fmaxf(cm, red[i]);
+            dm = fmaxf(dm, red[16 + i]);
+        }
         float omax = cm;
-        if (dm > cm) {  // uniform: every wave computed the same cm, dm
-            __syncthreads();  // every wave's band_max reads are done
+        if (dm > cm) {
             for (int k = w; k < a.nbt; k += NW) {
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;
                 const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
@@ -540,9 +551,16 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 }
             }
             __syncthreads();
-            trow.rebuild(w, NW, lane);
+            float m2 = 0.f;
+            for (int k = tid; k < a.nbt; k += NT)
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
+            m2 = wave_max(m2);
             __syncthreads();
-            omax = trow.clean_max(lane);
+            if (lane == 0) red[w] = m2;
+            __syncthreads();
+            omax = red[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
         }
         FPM_STAMP(9)
         const float rom = 1.0f / omax;
@@ -603,8 +621,7 @@ size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
     const int tld = fz::NP / ks + 1;
     return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
            48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
-           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int) +
-           2 * kMaxBandRows * sizeof(float);
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
 
 // distributed-mode area (float2 elements) for B patches
@@ -668,7 +685,6 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     a.nbx = bd.nbx;
     a.nbt = bd.nbt;
     a.rnbx = 1.0f / (float)a.nbx;
-    if (a.nbt / a.nbx > kMaxBandRows) return hipErrorInvalidValue;
     a.dbg = dbg;
     a.xch = area;
     a.flags = flags;

@@ -31,7 +31,6 @@
 #include "dft90.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
-#include "tilemax.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -93,8 +92,6 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     int *rowoff = (int *)(red + 48);           // 90: T offset of FFT row y (the zero row outside the box)
     float *tmx = (float *)(rowoff + NP);       // nbt band-tile maxima
     unsigned *dirty = (unsigned *)(tmx + a.nbt);
-    float *rowc = (float *)(dirty + ((a.nbt + 31) >> 5));  // kMaxBandRows: clean maximum per band tile row
-    float *rowd = rowc + kMaxBandRows;         // kMaxBandRows: dirty bound per band tile row
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int gw = lane / N2;                  // group within the wave (6 = idle lanes)
@@ -140,9 +137,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         inmask |= (in ? 1u : 0u) << k;
         P[k] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
-    __syncthreads();  // rowoff, tw; tile maxima and dirty bits
-    const TileRows trow{tmx, dirty, rowc, rowd, a.nbx, a.nbt / a.nbx};
-    trow.rebuild(w, NW, lane);  // read after the next LED's barriers
+    __syncthreads();  // rowoff, tw
     // column pass: T row offset of this lane's layout-A FFT row y = l + 10 k
     // (zero row outside the box), looked up per use (registers are short)
     auto roff = [&](int k) { return rowoff[l + 10 * k]; };
@@ -286,13 +281,29 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         }
         FPM_STAMP(4)
 
-        // ---- exact max|objF| (:460,467): per-tile-row maxima (tilemax.hpp),
-        // every wave forms the band's maxima itself -- no barrier on this path
-        float cm, dm;
-        trow.band_max(((yc - R) >> 4) - a.bty0, ((yc + R) >> 4) - a.bty0, w, NW, lane, cm, dm);
+        // ---- exact max|objF| (:460,467) from the band-tile maxima
+        float cm = 0.f, dm = 0.f;
+        for (int k = tid; k < a.nbt; k += NT) {
+            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
+            if (d) dm = fmaxf(dm, tmx[k]);
+            else cm = fmaxf(cm, tmx[k]);
+        }
+        cm = wave_max(cm);
+        dm = wave_max(dm);
+        if (lane == 0) {
+            red[w] = cm;
+            red[16 + w] = dm;
+        }
+        __syncthreads();
+        cm = red[0];
+        dm = red[16];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            cm = fmaxf(cm, red[i]);
+            dm = fmaxf(dm, red[16 + i]);
+        }
         float omax = cm;
-        if (dm > cm) {  // uniform: every wave computed the same cm, dm
-            __syncthreads();  // every wave's band_max reads are done
+        if (dm > cm) {  // block-uniform
             for (int k = w; k < a.nbt; k += NW) {
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;  // wave-uniform
                 const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
@@ -310,9 +321,16 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
                 }
             }
             __syncthreads();
-            trow.rebuild(w, NW, lane);
+            float m2 = 0.f;
+            for (int k = tid; k < a.nbt; k += NT)
+                if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
+            m2 = wave_max(m2);
             __syncthreads();
-            omax = trow.clean_max(lane);
+            if (lane == 0) red[w] = m2;
+            __syncthreads();
+            omax = red[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) omax = fmaxf(omax, red[i]);
         }
         FPM_STAMP(5)
         const float rom = 1.0f / omax;
@@ -358,8 +376,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
 namespace {
 size_t s90_lds_bytes(int nb, int nbt, int xw, int tld) {
     return (size_t)(f90::NW * xw + (nb + 2) * tld + 100) * sizeof(float2) + 48 * sizeof(float) +
-           f90::NP * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) +
-           2 * kMaxBandRows * sizeof(float);
+           f90::NP * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
 }
 }  // namespace
 
@@ -370,7 +387,6 @@ bool fused_s90_supported(int np, int r, const DevState &st) {
         return false;
     const int bty0 = st.sy0 / kTile, btx0 = st.sx0 / kTile;
     const int nbx = st.sx1 / kTile - btx0 + 1, nbt = nbx * (st.sy1 / kTile - bty0 + 1);
-    if (nbt / nbx > kMaxBandRows) return false;  // tilemax.hpp row maxima
     return s90_lds_bytes(2 * r + 1, nbt, f90::XW_DENSE, f90::TLD) <= 160 * 1024;
 }
 
