@@ -42,6 +42,7 @@
 #include "fused256.hpp"
 #include "fused_common.hpp"
 #include "fused_sync.hpp"
+#include "ledtab.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -168,7 +169,11 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             P[j][s] = in ? pup[(kyr[j] + R) * NB + kx + R] : make_float2(0.f, 0.f);
         }
     }
-    __syncthreads();  // tpx / tky / sig
+    // the launch's LED order as an LDS table (ledtab.hpp)
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
+    __syncthreads();  // tpx / tky / sig; LED table
     // per-lane half-T row offsets of this lane's six column slots; rows
     // outside the box read the zero row `nrows` and write the dummy row after it
     const int zoff = nrows * TLD;
@@ -284,8 +289,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     // for the second half's pass A and the object update, and right after the
     // object update for the next LED's first pass A.
     auto window = [&](int itn) {
-        const int ln = a.order[itn];
-        return spec + (unsigned)((a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2);
+        const LedPos p = lt.at(itn);
+        return spec + (unsigned)(p.yc * L + p.xc);
     };
     // slot s of row j sits at a compile-time offset from the lane's row base
     // (kx = t + 16 SK[s] - Np [s >= 3]), so one base register serves all six
@@ -304,8 +309,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         if (towner) Ot = sr[tp.x * L + tp.y];
     }
     for (int it = 0; it < a.n_order; ++it) {
-        const int led = a.order[it];
-        const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
+        const LedPos lp = lt.at(it);
+        const int led = lp.led, xc = lp.xc, yc = lp.yc;
         float2 *srow = spec + (unsigned)(yc * L + xc);   // spec[yc + ky][xc + kx] = srow[ky*L + kx]
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
 
@@ -823,8 +828,10 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     a.flags = ks > 1 ? flags : nullptr;
     a.abort_flag = ks > 1 ? flags + ks * st.B : nullptr;
     a.stall_led = ks > 1 ? stall_led : -1;
-    const size_t lds = fused_lds_bytes(ks, a.nbt, g.n_tail_rows);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const size_t lds0 = fused_lds_bytes(ks, a.nbt, g.n_tail_rows);
+    if (lds0 > 160 * 1024) return hipErrorInvalidValue;
+    size_t lds;  // + the LED table when it fits
+    a.ledtab_off = ledtab_offset(lds0, n_order, 160 * 1024, lds);
     const void *fn = ks == 4   ? (const void *)k_fused_iteration<512, 4>
                      : ks == 2 ? (const void *)k_fused_iteration<512, 2>
                                : (const void *)k_fused_iteration<512, 1>;

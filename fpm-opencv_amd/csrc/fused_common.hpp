@@ -46,6 +46,7 @@ struct FusedArgs {
                                 // then the abort flag, then [B][KS] XCC_ID + 1 of each part
     int *abort_flag;            // a handoff timed out: every workgroup leaves.  Sticky: the
                                 // per-launch reset does not clear it, fpm_run reports it
+    int ledtab_off;             // byte offset of the LED table in dynamic LDS (ledtab.hpp), or -1
     int stall_led;              // fpm_debug_set_stall (tests only): the last part stops
                                 // publishing from this LED on, forcing the timeout path; -1 off
 };

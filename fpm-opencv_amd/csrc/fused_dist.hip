@@ -43,6 +43,7 @@
 #include "fused256.hpp"
 #include "fused_common.hpp"
 #include "fused_sync.hpp"
+#include "ledtab.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -149,7 +150,11 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         inmask |= (in ? 1u : 0u) << s;
         P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
-    __syncthreads();  // tpx / tpq / sig
+    // the launch's LED order as an LDS table (ledtab.hpp)
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
+    __syncthreads();  // tpx / tpq / sig; LED table
     const int zoff = nrows * TLD;
     int roff[6];
 #pragma unroll
@@ -235,8 +240,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     auto soff = [](int s) { return 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); };
     // window of LED `itn` in the centred spectrum: element offset of (ky, kx) = (0, 0)
     auto wbase = [&](int itn) {
-        const int ln = a.order[itn];
-        return (a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2;
+        const LedPos p = lt.at(itn);
+        return p.yc * L + p.xc;
     };
     float2 Opre[6];
     auto load_window = [&](int itn) {
@@ -252,8 +257,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 
     for (int it = 0; it < a.n_order; ++it) {
         cur = it;
-        const int led = a.order[it];
-        const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
+        const LedPos lp = lt.at(it);
+        const int led = lp.led, xc = lp.xc, yc = lp.yc;
         const int wb0 = yc * L + xc;
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         Tw wt;
@@ -426,12 +431,18 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             if ((tpq[pp] % KS) != hown) continue;  // group-uniform
             const int2 px = tpx[pp];
             const int row = NROWS + tpq[pp];
+            // the row's 16 values first: one L2 round trip (loads interleaved
+            // with the twiddle recurrence waited for each in turn, 16 round
+            // trips on every part that owns a tail row)
+            float2 e[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) e[m] = cld(ra, row * NP + t + 16 * m);
             pf2 s2p = {0.f, 0.f};
             pf2 wk = pin(tw[(t * (px.y + NP)) & (NP - 1)]);
             const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
-                s2p += pmul(pin(cld(ra, row * NP + t + 16 * m)), wk);
+                s2p += pmul(pin(e[m]), wk);
                 if (m < 15) wk = pmul(wk, wstep);
             }
             float2 s2 = pout(s2p);
@@ -497,14 +508,18 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
         if (ti < wnt) {
             const int bk = wtile(ti);
+            // every partner's tile is loaded before the first is used: one L2
+            // round trip (the load-use loop waited for each in turn, KS - 1
+            // round trips)
+            float2 e[KS - 1];
+#pragma unroll
+            for (int q = 0; q < KS - 1; ++q) e[q] = cld(ra, TILES_OFF + (q < hown ? q : q + 1) * kWinTiles + ti);
             float m = tmx[bk];
             unsigned d = 0;
 #pragma unroll
-            for (int p = 0; p < KS; ++p) {
-                if (p == hown) continue;
-                const float2 e = cld(ra, TILES_OFF + p * kWinTiles + ti);
-                m = fmaxf(m, e.x);
-                d |= __float_as_uint(e.y);
+            for (int q = 0; q < KS - 1; ++q) {
+                m = fmaxf(m, e[q].x);
+                d |= __float_as_uint(e[q].y);
             }
             tmx[bk] = m;
             if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
@@ -690,8 +705,10 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     a.flags = flags;
     a.abort_flag = flags + ks * st.B;
     a.stall_led = stall_led;
-    const size_t lds = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const size_t lds0 = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
+    if (lds0 > 160 * 1024) return hipErrorInvalidValue;
+    size_t lds;  // + the LED table when it fits
+    a.ledtab_off = ledtab_offset(lds0, n_order, 160 * 1024, lds);
     const void *fn = ks == 8   ? (const void *)k_fused_dist<8>
                      : ks == 4 ? (const void *)k_fused_dist<4>
                                : (const void *)k_fused_dist<2>;

@@ -39,6 +39,7 @@
 #include "dft200.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
+#include "ledtab.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -89,6 +90,7 @@ struct FusedMRArgs {
     int xw;                    // exchange tiles: wave slot (complex)
     int xg[fm::GPW];           // tile offset of group gw in the wave slot
     int tld;                   // T row pitch (complex): TLD_FAST or fm::TLD
+    int ledtab_off;            // LED table in dynamic LDS (ledtab.hpp), or -1
 };
 
 __device__ __forceinline__ int mr_slot_k(int s) { return fm::SK[s]; }
@@ -154,6 +156,10 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         inmask |= (in ? 1u : 0u) << s;
         P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
+    // the launch's LED order as an LDS table (ledtab.hpp)
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
     __syncthreads();  // sig, tw2
     // T row offsets of this lane's six column slots (zero row outside the box)
     int roff[6];
@@ -176,8 +182,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         prev = now_;                                                  \
     }
     auto window = [&](int itn) {
-        const int ln = a.order[itn];
-        return spec + (unsigned)((a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2);
+        const LedPos p = lt.at(itn);
+        return spec + (unsigned)(p.yc * L + p.xc);
     };
     // slot s of this lane's box row at a compile-time offset from one base
     auto soff = [](int s) { return 10 * fm::SK[s] - (fm::SK[s] >= 10 ? fm::NP : 0); };
@@ -192,8 +198,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         for (int s = 0; s < 6; ++s) Opre[s] = ldO(sr, s);
     }
     for (int it = 0; it < a.n_order; ++it) {
-        const int led = a.order[it];
-        const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
+        const LedPos lp = lt.at(it);
+        const int led = lp.led, xc = lp.xc, yc = lp.yc;
         float2 *srow = spec + (unsigned)(yc * L + xc);
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[20];
@@ -450,7 +456,8 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
     a.xw = fits(fm::XW_SHIFT, a.tld) ? fm::XW_SHIFT : fits(fm::XW_STRIDE, a.tld) ? fm::XW_STRIDE : fm::XW_DENSE;
     for (int i = 0; i < fm::GPW; ++i)
         a.xg[i] = a.xw == fm::XW_SHIFT ? fm::XG_SHIFT[i] : i * (a.xw == fm::XW_STRIDE ? 106 : fm::XT);
-    const size_t lds = mr_lds_bytes(st.nb, a.nbt, a.xw, a.tld);
+    size_t lds;  // the kernel's own LDS + the LED table when it fits
+    a.ledtab_off = ledtab_offset(mr_lds_bytes(st.nb, a.nbt, a.xw, a.tld), n_order, 160 * 1024, lds);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_mr, dim3(st.B), dim3(fm::NT), lds, s, a);

@@ -31,6 +31,7 @@
 #include "dft90.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
+#include "ledtab.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -73,6 +74,7 @@ struct FusedS90Args {
     int xw;                    // exchange tiles: wave slot (complex)
     int xg[f90::GPW];          // tile offset of group gw in the wave slot
     int tld;                   // T row pitch (complex)
+    int ledtab_off;            // LED table in dynamic LDS (ledtab.hpp), or -1
     unsigned long long *dbg;   // FPM_STAMPS=1 phase cycles (fused_mr.hip's slots), else null
 };
 
@@ -137,6 +139,10 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         inmask |= (in ? 1u : 0u) << k;
         P[k] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
+    // the launch's LED order as an LDS table (ledtab.hpp)
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
     __syncthreads();  // rowoff, tw
     // column pass: T row offset of this lane's layout-A FFT row y = l + 10 k
     // (zero row outside the box), looked up per use (registers are short)
@@ -147,8 +153,8 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     const float epsn_im = st.eps_im * (float)(NP * NP);
 
     auto window = [&](int itn) {
-        const int ln = a.order[itn];
-        return spec + (unsigned)((a.y0[ln] + NP / 2) * L + a.x0[ln] + NP / 2);
+        const LedPos p = lt.at(itn);
+        return spec + (unsigned)(p.yc * L + p.xc);
     };
     auto ldO = [&](const float2 *sr, int k) {
         return ((inmask >> k) & 1) ? sr[kyr * L + f90_fold(l + 10 * k)] : make_float2(0.f, 0.f);
@@ -176,8 +182,8 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         prev = now_;                                                  \
     }
     for (int it = 0; it < a.n_order; ++it) {
-        const int led = a.order[it];
-        const int xc = a.x0[led] + NP / 2, yc = a.y0[led] + NP / 2;
+        const LedPos lp = lt.at(it);
+        const int led = lp.led, xc = lp.xc, yc = lp.yc;
         float2 *srow = spec + (unsigned)(yc * L + xc);
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[10];
@@ -413,7 +419,8 @@ hipError_t launch_fused_s90_iteration(const DevState &st, const uint16_t *meas, 
     for (int i = 0; i < f90::GPW; ++i) a.xg[i] = fast ? f90::XG_FAST[i] : i * f90::XT;
     a.tld = fast ? f90::TLD_FAST : f90::TLD;
     a.dbg = dbg;
-    const size_t lds = s90_lds_bytes(st.nb, a.nbt, a.xw, a.tld);
+    size_t lds;  // the kernel's own LDS + the LED table when it fits
+    a.ledtab_off = ledtab_offset(s90_lds_bytes(st.nb, a.nbt, a.xw, a.tld), n_order, 160 * 1024, lds);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_s90, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_s90, dim3(st.B), dim3(f90::NT), lds, s, a);
