@@ -96,6 +96,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * XTILE;
     const int nwords = (a.nbt + 31) >> 5;
+    // spread object update (KS 8): F, O, P of the own rows' slots staged in
+    // the exchange tiles of the groups that own no FFT row (free in C and the
+    // update).  32-patch shard 2.74 -> 2.83 M (update 3.6k -> 2.2k cycles per
+    // LED); at KS 4 (four owner waves) the staging stores in C cost what the
+    // spread saved (64-patch shard 4.16 vs 4.10 M), profiles/r05_ab/dist_max_upd_ab.txt
+    constexpr bool kSpreadUpd = KS == 8;
+    static_assert(!kSpreadUpd || 3 * NOWN * 96 <= (NG - NOWN) * XTILE, "staging fits the idle groups' tiles");
+    float2 *upd_f = scr_all + NOWN * XTILE, *upd_o = upd_f + NOWN * 96, *upd_p = upd_o + NOWN * 96;
     constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
 
     // ---- one-time setup
@@ -221,13 +229,21 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     int sync_no = 0;  // handoffs of this launch (flag values are 1, 2, 3, ...)
     bool aborted = false;
     int cur = 0;      // LED position of the handoffs below
-    auto handoff = [&]() {
+    // idle(): work for waves 1 .. NW-1 while the first wave polls the
+    // partners' flags (this part's flag is already out)
+    auto handoff = [&](auto &&idle) {
         ++sync_no;
         // fault injection (fpm_debug_set_stall): the last part stops
         // publishing from LED position stall_led on, its partners time out
         if (a.stall_led < 0 || cur < a.stall_led || hown != KS - 1) handoff_publish(flg + hown, sync_no, local);
+        if (w > 0) idle();
         return handoff_wait<KS>(flg, hown, sync_no, a.abort_flag, ccnt + 1, local, rf);
     };
+    auto nothing = []() {};
+    // exact max|objF| (:460,467): the window's tiles are merged on one wave
+    // (the last at KS 8, where thread NT-1-k merges tile k; else the first)
+    constexpr int WMERGE = KS == 8 ? NW - 1 : 0;
+    unsigned *omx = (unsigned *)(red + 40);  // [0] clean / [1] dirty max over the tiles outside the window
 
     unsigned long long acc[kStamps] = {};
     unsigned long long prev = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -267,6 +283,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 
         // ---- gather + A: row IDFTs of the own rows, all 256 outputs to Tg (:358-365)
         if (towner) tailX[ti] = pout(pmul(pin(Ot), pin(Pt)));
+        if (tid == 0) omx[0] = omx[1] = 0u;  // read by the previous LED's merge, two barriers ago
         __syncthreads();  // tailX
         FPM_STAMP(0)
         if (g < NOWN) {  // group-uniform
@@ -309,7 +326,28 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             for (int i = 1; i < NW; ++i) m2 = fmaxf(m2, red[32 + i]);
             cst(ra, PMX_OFF + hown, make_float2(m2, 0.f));
         }
-        if (!handoff()) {
+        // while the first wave polls: the max over the band tiles OUTSIDE this
+        // LED's window (no part's update touches them) on waves 1 .. NW-1,
+        // folded into omx by LDS atomics (float bits of values >= 0 order as
+        // unsigned)
+        const int wty0 = (yc - R) >> 4, wtx0 = (xc - R) >> 4;
+        const int wty1 = (yc + R) >> 4, wtx1 = (xc + R) >> 4;
+        if (!handoff([&]() {
+                float c = 0.f, d = 0.f;
+                for (int k = tid - 64; k < a.nbt; k += NT - 64) {
+                    const int dy = band_dy(k), ty = a.bty0 + dy, tx = a.btx0 + k - dy * a.nbx;
+                    if (ty >= wty0 && ty <= wty1 && tx >= wtx0 && tx <= wtx1) continue;
+                    const float v = tmx[k];
+                    if ((dirty[k >> 5] >> (k & 31)) & 1u) d = fmaxf(d, v);
+                    else c = fmaxf(c, v);
+                }
+                c = wave_max(c);
+                d = wave_max(d);
+                if (lane == 0) {
+                    atomicMax(&omx[0], __float_as_uint(c));
+                    atomicMax(&omx[1], __float_as_uint(d));
+                }
+            })) {
             aborted = true;
             break;
         }
@@ -403,7 +441,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             else __builtin_amdgcn_raw_buffer_store_b128(d, ra, off, 0, 16);
         }
         FPM_STAMP(3)
-        if (!handoff()) {  // ---- sync 2
+        if (!handoff(nothing)) {  // ---- sync 2
             aborted = true;
             break;
         }
@@ -418,6 +456,17 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 #ifdef FPM_DIST_SUBSTAMP
             FPM_STAMP(11)  // C: own FFT rows (waves with rows)
 #endif
+            if constexpr (kSpreadUpd) {
+                // stage F, O, P of the row's slots for the spread update below
+                // in the idle groups' exchange tiles (no transform uses them in C)
+#pragma unroll
+                for (int s = 0; s < 6; ++s) {
+                    const int i = (g * 6 + s) * 16 + t;
+                    upd_f[i] = F[s];
+                    upd_o[i] = Opre[s];
+                    upd_p[i] = P[s];
+                }
+            }
         } else {
 #pragma unroll
             for (int s = 0; s < 6; ++s) F[s] = make_float2(0.f, 0.f);
@@ -460,7 +509,27 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             if (an < ao && cur <= __float_as_uint(ao)) atomicOr(&dirty[ti >> 5], 1u << (ti & 31));
             if (__float_as_uint(an) > cur) atomicMax(&tmu[ti], __float_as_uint(an));
         };
-        if (ron) {  // support pixels only (a slot off the disk in the whole wave is skipped)
+        if constexpr (kSpreadUpd) {
+            // the own rows' NOWN x 96 slots spread over all NT threads (the
+            // row owners are NOWN / 4 waves, one per SIMD at KS 8: six
+            // updates per lane at the one-wave issue rate); numerators into
+            // the owner group's exchange tile as before
+#pragma unroll
+            for (int j = 0; j < (NOWN * 96 + NT - 1) / NT; ++j) {
+                const int i = tid + NT * j;
+                if (NOWN * 96 % NT != 0 && i >= NOWN * 96) break;
+                const int gi = i / 96, si = (i - gi * 96) >> 4, tt = i & 15;
+                const int rowi = hown + KS * gi, ky = a.ky_lo + rowi, kx = slot_kx(tt, si);
+                float2 num = make_float2(0.f, 0.f);
+                if (rowi < a.n_fft_rows && ky * ky + kx * kx <= R * R) {
+                    float oa;
+                    const float2 nv = slot_update(upd_f[i], upd_o[i], upd_p[i], pm, st, num, oa);
+                    cst(rs, wb0 + ky * L + kx, nv);
+                    note(yc + ky, xc + kx, oa, cmag(nv));
+                }
+                scr_all[gi * XTILE + si * 16 + tt] = num;
+            }
+        } else if (ron) {  // support pixels only (a slot off the disk in the whole wave is skipped)
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
                 float2 num = make_float2(0.f, 0.f);
@@ -481,8 +550,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         __syncthreads();  // tile maxima of this part's pixels
         // publish the window's tiles (the only ones any part changed)
-        const int wty0 = (yc - R) >> 4, wtx0 = (xc - R) >> 4;
-        const int wnx = ((xc + R) >> 4) - wtx0 + 1, wnt = wnx * (((yc + R) >> 4) - wty0 + 1);
+        const int wnx = wtx1 - wtx0 + 1, wnt = wnx * (wty1 - wty0 + 1);
         auto wtile = [&](int k) {  // band index of window tile k
             const int dy = k / wnx;
             return (wty0 + dy - a.bty0) * a.nbx + (wtx0 + k - dy * wnx - a.btx0);
@@ -498,7 +566,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         __builtin_amdgcn_s_waitcnt(0);  // this wave's spectrum / tile stores acknowledged
         FPM_STAMP(12)
 #endif
-        if (!handoff()) {  // ---- sync 3
+        if (!handoff(nothing)) {  // ---- sync 3
             aborted = true;
             break;
         }
@@ -506,6 +574,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // the next window first (its loads overlap the merge), then the
         // merge: every part ends with the same maxima and dirty bits
         if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
+        float wcm = 0.f;      // merged window tile of this thread (ti < wnt)
+        bool wdirty = false;
         if (ti < wnt) {
             const int bk = wtile(ti);
             // every partner's tile is loaded before the first is used: one L2
@@ -523,42 +593,39 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             }
             tmx[bk] = m;
             if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
+            wcm = m;
+            wdirty = d || ((dirty[bk >> 5] >> (bk & 31)) & 1u);
+        }
+        // the merge wave folds the window tiles into the outside maxima
+        if (w == WMERGE) {
+            float c = wdirty ? 0.f : wcm, d = wdirty ? wcm : 0.f;
+            c = wave_max(c);
+            d = wave_max(d);
+            if (lane == 0) {
+                red[0] = fmaxf(c, __uint_as_float(omx[0]));
+                red[16] = fmaxf(d, __uint_as_float(omx[1]));
+            }
         }
         __syncthreads();
         FPM_STAMP(8)
 
-        // ---- exact max|objF| (:460,467), identical in every part
-        float cm = 0.f, dm = 0.f;
-        for (int k = tid; k < a.nbt; k += NT) {
-            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
-            if (d) dm = fmaxf(dm, tmx[k]);
-            else cm = fmaxf(cm, tmx[k]);
-        }
-        cm = wave_max(cm);
-        dm = wave_max(dm);
-        if (lane == 0) {
-            red[w] = cm;
-            red[16 + w] = dm;
-        }
-        __syncthreads();
-        cm = red[0];
-        dm = red[16];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) {
-            cm = fmaxf(cm, red[i]);
-            dm = fmaxf(dm, red[16 + i]);
-        }
+        // ---- exact max|objF| (:460,467), identical in every part: the
+        // outside maxima of sync 1 and the merged window tiles
+        const float cm = red[0], dm = red[16];
         float omax = cm;
         if (dm > cm) {
             for (int k = w; k < a.nbt; k += NW) {
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;
                 const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
-                float mm = 0.f;
+                float2 e[4];  // all four loads before the first use
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int pp = lane + 64 * jj;
-                    mm = fmaxf(mm, cmag(cld(rs, (ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15))));
+                    e[jj] = cld(rs, (ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15));
                 }
+                float mm = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) mm = fmaxf(mm, cmag(e[jj]));
                 mm = wave_max(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
@@ -616,7 +683,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             for (int i = 1; i < NW; ++i) m2 = fmaxf(m2, red[32 + i]);
             cst(ra, PMX_OFF + hown, make_float2(m2, 0.f));
         }
-        if (handoff() && hown == 0 && tid == 0) {
+        if (handoff(nothing) && hown == 0 && tid == 0) {
             float m2 = 0.f;
 #pragma unroll
             for (int p = 0; p < KS; ++p) m2 = fmaxf(m2, cld(ra, PMX_OFF + p).x);
