@@ -40,6 +40,7 @@
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
 #include "ledtab.hpp"
+#include "tilemax.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -54,6 +55,7 @@ constexpr int NW = NT / 64;
 constexpr int NG = NW * GPW;              // 72 groups >= box rows (r <= 35)
 constexpr int SK[6] = {0, 1, 2, 17, 18, 19};  // registers that can hold |k| <= 29
 constexpr int RMAX = 29;
+static_assert((2 * RMAX + 1 + GPW - 1) / GPW < NW, "a wave with no box row (tilemax.hpp)");
 static_assert(NG >= 2 * RMAX + 1, "one group per box row");
 constexpr int KYOFF = 32;                 // sig table covers ky in [-32, 31]
 constexpr int XP = 10;                    // exchange-tile row pitch (complex)
@@ -146,6 +148,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     float2 *pup = st.pupil + (size_t)b * NB * NB;
     // box row of this group (all box rows are transformed: NG >= NB)
     const bool ron = act && g < NB;
+    const int wi0 = (NB + GPW - 1) / GPW;  // first wave with no box row (< NW: r <= RMAX)
     const int kyr = g - R;
     unsigned inmask = 0;
     float2 P[6];
@@ -200,6 +203,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     for (int it = 0; it < a.n_order; ++it) {
         const LedPos lp = lt.at(it);
         const int led = lp.led, xc = lp.xc, yc = lp.yc;
+        const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // the band tiles this LED's update touches
         float2 *srow = spec + (unsigned)(yc * L + xc);
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[20];
@@ -310,8 +314,18 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
                 th[g * TLD + s * 10 + l] = num;
             }
         }
+        // the waves with no box row (idle in C and the update): max over the
+        // band tiles outside this LED's window, which no update touches
+        if (w >= wi0) {
+            float c, d;
+            outside_max(tmx, dirty, a.nbt, a.nbx, a.rnbx, wn, tid - 64 * wi0, NT - 64 * wi0, c, d);
+            if (lane == 0) {
+                red[w] = c;
+                red[16 + w] = d;
+            }
+        }
         FPM_STAMP(9)
-        __syncthreads();  // spectrum writes, tile maxima, dirty bits
+        __syncthreads();  // spectrum writes, tile maxima, dirty bits; outside maxima
         if (it + 1 < a.n_order) {
             const float2 *sr = window(it + 1);
 #pragma unroll
@@ -320,26 +334,23 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         FPM_STAMP(4)
 
         // ---- exact max|objF| (:460,467) from the band-tile maxima
-        float cm = 0.f, dm = 0.f;
-        for (int k = tid; k < a.nbt; k += NT) {
-            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
-            if (d) dm = fmaxf(dm, tmx[k]);
-            else cm = fmaxf(cm, tmx[k]);
-        }
-        cm = wave_max(cm);
-        dm = wave_max(dm);
-        if (lane == 0) {
-            red[w] = cm;
-            red[16 + w] = dm;
+        // the last wave folds the window tiles into the outside maxima
+        // (tilemax.hpp) and hands them over through one barrier
+        if (w == NW - 1) {
+            float c0 = red[wi0], d0 = red[16 + wi0];
+            for (int i = wi0 + 1; i < NW; ++i) {
+                c0 = fmaxf(c0, red[i]);
+                d0 = fmaxf(d0, red[16 + i]);
+            }
+            float c, d;
+            window_max(tmx, dirty, a.nbx, wn, lane, c0, d0, c, d);
+            if (lane == 0) {
+                red[0] = c;
+                red[16] = d;
+            }
         }
         __syncthreads();
-        cm = red[0];
-        dm = red[16];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) {
-            cm = fmaxf(cm, red[i]);
-            dm = fmaxf(dm, red[16 + i]);
-        }
+        const float cm = red[0], dm = red[16];
         float omax = cm;
         if (dm > cm) {  // block-uniform
             for (int k = w; k < a.nbt; k += NW) {

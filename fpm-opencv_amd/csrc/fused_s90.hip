@@ -32,6 +32,7 @@
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
 #include "ledtab.hpp"
+#include "tilemax.hpp"
 #include "update.hpp"
 
 namespace fpm {
@@ -61,6 +62,7 @@ constexpr int XW_FAST = 704;
 constexpr int XG_FAST[GPW] = {0, 122, 230, 356, 478, 602};
 constexpr int TLD_FAST = 106;
 constexpr int RMAX = 44;               // 2 r + 1 <= Np
+static_assert((2 * RMAX + 1 + GPW - 1) / GPW < NW, "a wave with no box row (tilemax.hpp)");
 }  // namespace f90
 
 struct FusedS90Args {
@@ -129,6 +131,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     float2 *pup = st.pupil + (size_t)b * NB * NB;
     // box row of this group, its nine layout-A pixels kx = fold(l + 10 k)
     const bool ron = act && g < NB;
+    const int wi0 = (NB + GPW - 1) / GPW;  // first wave with no box row (< NW: r <= RMAX)
     const int kyr = g - R;
     unsigned inmask = 0;
     float2 P[9];
@@ -184,6 +187,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     for (int it = 0; it < a.n_order; ++it) {
         const LedPos lp = lt.at(it);
         const int led = lp.led, xc = lp.xc, yc = lp.yc;
+        const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // the band tiles this LED's update touches
         float2 *srow = spec + (unsigned)(yc * L + xc);
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[10];
@@ -278,8 +282,18 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
                 note(yc + kyr, xc + kx, oa, cmag(nv));
             }
         }
+        // the waves with no box row (idle in C and the update): max over the
+        // band tiles outside this LED's window, which no update touches
+        if (w >= wi0) {
+            float c, d;
+            outside_max(tmx, dirty, a.nbt, a.nbx, a.rnbx, wn, tid - 64 * wi0, NT - 64 * wi0, c, d);
+            if (lane == 0) {
+                red[w] = c;
+                red[16 + w] = d;
+            }
+        }
         FPM_STAMP(9)
-        __syncthreads();  // spectrum writes, tile maxima, dirty bits
+        __syncthreads();  // spectrum writes, tile maxima, dirty bits; outside maxima
         if (it + 1 < a.n_order) {
             const float2 *sr = window(it + 1);
 #pragma unroll
@@ -288,26 +302,23 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         FPM_STAMP(4)
 
         // ---- exact max|objF| (:460,467) from the band-tile maxima
-        float cm = 0.f, dm = 0.f;
-        for (int k = tid; k < a.nbt; k += NT) {
-            const bool d = (dirty[k >> 5] >> (k & 31)) & 1u;
-            if (d) dm = fmaxf(dm, tmx[k]);
-            else cm = fmaxf(cm, tmx[k]);
-        }
-        cm = wave_max(cm);
-        dm = wave_max(dm);
-        if (lane == 0) {
-            red[w] = cm;
-            red[16 + w] = dm;
+        // the last wave folds the window tiles into the outside maxima
+        // (tilemax.hpp) and hands them over through one barrier
+        if (w == NW - 1) {
+            float c0 = red[wi0], d0 = red[16 + wi0];
+            for (int i = wi0 + 1; i < NW; ++i) {
+                c0 = fmaxf(c0, red[i]);
+                d0 = fmaxf(d0, red[16 + i]);
+            }
+            float c, d;
+            window_max(tmx, dirty, a.nbx, wn, lane, c0, d0, c, d);
+            if (lane == 0) {
+                red[0] = c;
+                red[16] = d;
+            }
         }
         __syncthreads();
-        cm = red[0];
-        dm = red[16];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) {
-            cm = fmaxf(cm, red[i]);
-            dm = fmaxf(dm, red[16 + i]);
-        }
+        const float cm = red[0], dm = red[16];
         float omax = cm;
         if (dm > cm) {  // block-uniform
             for (int k = w; k < a.nbt; k += NW) {
