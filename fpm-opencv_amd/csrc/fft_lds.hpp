@@ -15,6 +15,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace fpm {
 
 struct FftPlan {
@@ -341,16 +343,25 @@ __device__ __forceinline__ float row16_sum(float v) {
     v += dpp_f<0x121>(v);  // row_ror:1
     return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-    v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
-    v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
-    v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror: the other quad of the 8
-    v = fmaxf(v, dpp_f<0x140>(v));  // row_mirror: the other 8 of the row
-    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
-    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
-    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+// Every caller reduces values >= +0 (magnitudes, |z|^2, tile maxima), whose
+// IEEE bits order as unsigned integers: the steps are v_max_u32 (fmaxf costs a
+// canonicalising v_max per operand in IEEE mode: three VALU per step instead
+// of one) and the four row maxima fold on the scalar unit.  A NaN would win
+// here where fmaxf drops it -- it never reaches a maximum of a finite run.
+__device__ __forceinline__ float wave_max(float x) {
+    unsigned v = __float_as_uint(x);
+    auto dpp_u = [](unsigned u, auto ctrl) {
+        // old = 0, the identity of unsigned max: the DPP combiner folds the
+        // move into the v_max_u32 that uses it
+        return (unsigned)__builtin_amdgcn_update_dpp(0, (int)u, decltype(ctrl)::value, 0xF, 0xF, false);
+    };
+    v = max(v, dpp_u(v, std::integral_constant<int, 0xB1>{}));   // quad_perm [1,0,3,2]: lane ^ 1
+    v = max(v, dpp_u(v, std::integral_constant<int, 0x4E>{}));   // quad_perm [2,3,0,1]: lane ^ 2
+    v = max(v, dpp_u(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror: the other quad of the 8
+    v = max(v, dpp_u(v, std::integral_constant<int, 0x140>{}));  // row_mirror: the other 8 of the row
+    const unsigned r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const unsigned r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return __uint_as_float(max(max(r0, r1), max(r2, r3)));
 }
 
 // Max over the block; `red` is LDS scratch of >= nwaves floats. Result valid

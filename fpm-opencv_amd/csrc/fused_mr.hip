@@ -108,7 +108,8 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     const int TLD = a.tld;
     float2 *th = tiles + NW * a.xw;            // (NB + 2) * TLD: T rows, zero row, dummy row
     float2 *tw2 = th + (NB + 2) * TLD;         // [m1][l] = W200^{l m1}
-    float *red = (float *)(tw2 + 200);         // 48
+    float *red = (float *)(tw2 + 200);         // 48: maxima per wave; [44..45] outside-window tile maxima
+    unsigned *omx = (unsigned *)(red + 44);
     int *sig = (int *)(red + 48);              // 64: T row of ky in [-32, 31], -1 outside the box
     float *tmx = (float *)(sig + 64);          // nbt band-tile maxima
     unsigned *dirty = (unsigned *)(tmx + a.nbt);
@@ -163,6 +164,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
     const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
     if (ltl) lt.fill(ltl, a.n_order, tid, NT);
+    if (tid == 0) omx[0] = omx[1] = 0u;
     __syncthreads();  // sig, tw2
     // T row offsets of this lane's six column slots (zero row outside the box)
     int roff[6];
@@ -203,7 +205,6 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     for (int it = 0; it < a.n_order; ++it) {
         const LedPos lp = lt.at(it);
         const int led = lp.led, xc = lp.xc, yc = lp.yc;
-        const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // the band tiles this LED's update touches
         float2 *srow = spec + (unsigned)(yc * L + xc);
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[20];
@@ -318,10 +319,11 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         // band tiles outside this LED's window, which no update touches
         if (w >= wi0) {
             float c, d;
+            const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // the band tiles this LED's update touches
             outside_max(tmx, dirty, a.nbt, a.nbx, a.rnbx, wn, tid - 64 * wi0, NT - 64 * wi0, c, d);
-            if (lane == 0) {
-                red[w] = c;
-                red[16 + w] = d;
+            if (lane == 0) {  // >= 0: the float bits order as unsigned
+                atomicMax(&omx[0], __float_as_uint(c));
+                atomicMax(&omx[1], __float_as_uint(d));
             }
         }
         FPM_STAMP(9)
@@ -337,16 +339,13 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         // the last wave folds the window tiles into the outside maxima
         // (tilemax.hpp) and hands them over through one barrier
         if (w == NW - 1) {
-            float c0 = red[wi0], d0 = red[16 + wi0];
-            for (int i = wi0 + 1; i < NW; ++i) {
-                c0 = fmaxf(c0, red[i]);
-                d0 = fmaxf(d0, red[16 + i]);
-            }
             float c, d;
-            window_max(tmx, dirty, a.nbx, wn, lane, c0, d0, c, d);
+            const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // (recomputed: registers are short)
+            window_max(tmx, dirty, a.nbx, wn, lane, __uint_as_float(omx[0]), __uint_as_float(omx[1]), c, d);
             if (lane == 0) {
                 red[0] = c;
                 red[16] = d;
+                omx[0] = omx[1] = 0u;  // the next LED's scans start after the barrier below
             }
         }
         __syncthreads();

@@ -92,8 +92,9 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     const int TLD = a.tld;
     float2 *th = tiles + NW * a.xw;            // (NB + 2) * TLD: T rows, zero row, dummy row
     float2 *tw = th + (NB + 2) * TLD;          // [a][b] = W90^{a b}, a, b < 10
-    float *red = (float *)(tw + 100);          // 48
-    int *rowoff = (int *)(red + 48);           // 90: T offset of FFT row y (the zero row outside the box)
+    float *red = (float *)(tw + 100);          // 52: maxima per wave; [48..49] outside-window tile maxima
+    unsigned *omx = (unsigned *)(red + 48);
+    int *rowoff = (int *)(red + 52);           // 90: T offset of FFT row y (the zero row outside the box)
     float *tmx = (float *)(rowoff + NP);       // nbt band-tile maxima
     unsigned *dirty = (unsigned *)(tmx + a.nbt);
 
@@ -146,6 +147,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
     const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
     if (ltl) lt.fill(ltl, a.n_order, tid, NT);
+    if (tid == 0) omx[0] = omx[1] = 0u;
     __syncthreads();  // rowoff, tw
     // column pass: T row offset of this lane's layout-A FFT row y = l + 10 k
     // (zero row outside the box), looked up per use (registers are short)
@@ -187,7 +189,6 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     for (int it = 0; it < a.n_order; ++it) {
         const LedPos lp = lt.at(it);
         const int led = lp.led, xc = lp.xc, yc = lp.yc;
-        const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // the band tiles this LED's update touches
         float2 *srow = spec + (unsigned)(yc * L + xc);
         const uint16_t *Ib = a.meas + ((size_t)led * st.B + b) * NP * NP;
         float2 v[10];
@@ -286,10 +287,11 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         // band tiles outside this LED's window, which no update touches
         if (w >= wi0) {
             float c, d;
+            const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // the band tiles this LED's update touches
             outside_max(tmx, dirty, a.nbt, a.nbx, a.rnbx, wn, tid - 64 * wi0, NT - 64 * wi0, c, d);
-            if (lane == 0) {
-                red[w] = c;
-                red[16 + w] = d;
+            if (lane == 0) {  // >= 0: the float bits order as unsigned
+                atomicMax(&omx[0], __float_as_uint(c));
+                atomicMax(&omx[1], __float_as_uint(d));
             }
         }
         FPM_STAMP(9)
@@ -305,16 +307,13 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         // the last wave folds the window tiles into the outside maxima
         // (tilemax.hpp) and hands them over through one barrier
         if (w == NW - 1) {
-            float c0 = red[wi0], d0 = red[16 + wi0];
-            for (int i = wi0 + 1; i < NW; ++i) {
-                c0 = fmaxf(c0, red[i]);
-                d0 = fmaxf(d0, red[16 + i]);
-            }
             float c, d;
-            window_max(tmx, dirty, a.nbx, wn, lane, c0, d0, c, d);
+            const TileWin wn = tile_window(yc, xc, R, a.bty0, a.btx0);  // (recomputed: registers are short)
+            window_max(tmx, dirty, a.nbx, wn, lane, __uint_as_float(omx[0]), __uint_as_float(omx[1]), c, d);
             if (lane == 0) {
                 red[0] = c;
                 red[16] = d;
+                omx[0] = omx[1] = 0u;  // the next LED's scans start after the barrier below
             }
         }
         __syncthreads();
@@ -392,7 +391,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
 // ------------------------------------------------------------------ host side
 namespace {
 size_t s90_lds_bytes(int nb, int nbt, int xw, int tld) {
-    return (size_t)(f90::NW * xw + (nb + 2) * tld + 100) * sizeof(float2) + 48 * sizeof(float) +
+    return (size_t)(f90::NW * xw + (nb + 2) * tld + 100) * sizeof(float2) + 52 * sizeof(float) +
            f90::NP * sizeof(int) + (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned);
 }
 }  // namespace

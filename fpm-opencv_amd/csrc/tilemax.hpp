@@ -55,16 +55,16 @@ __device__ __forceinline__ void outside_max(const float *tmx, const unsigned *di
 }
 
 // After the update (tiles final): the band's clean maximum cm and dirty
-// bound dm in every lane, from the window tiles and the partials c0 / d0 of
-// the tiles outside it (already folded over the scanning waves).
+// bound dm in every lane, from the window tiles and the maxima c0 / d0 of
+// the tiles outside it.  Lane 8 dy + dx takes window tile (dy, dx): the
+// window spans at most 8 x 8 tiles (2r + 1 <= 113 pixels; every fused kernel
+// has r <= 44).
 __device__ __forceinline__ void window_max(const float *tmx, const unsigned *dirty, int nbx, const TileWin &wn,
                                            int lane, float c0, float d0, float &cm, float &dm) {
     float cc = c0, dd = d0;
-    const int wnx = wn.nx(), wnt = wn.count();
-    const float rwnx = 1.0f / (float)wnx;
-    for (int i = lane; i < wnt; i += 64) {
-        const int dy = (int)(((float)i + 0.5f) * rwnx);  // i < 64: exact
-        const int k = (wn.y0 + dy) * nbx + wn.x0 + (i - dy * wnx);
+    const int dy = lane >> 3, dx = lane & 7;
+    if (dy <= wn.y1 - wn.y0 && dx < wn.nx()) {
+        const int k = (wn.y0 + dy) * nbx + wn.x0 + dx;
         const float v = tmx[k];
         if (tile_dirty(dirty, k)) dd = fmaxf(dd, v);
         else cc = fmaxf(cc, v);
