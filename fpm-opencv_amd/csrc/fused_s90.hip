@@ -313,7 +313,13 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
             if (lane == 0) {
                 red[0] = c;
                 red[16] = d;
-                omx[0] = omx[1] = 0u;  // the next LED's scans start after the barrier below
+                // the next LED's scans start after the barrier below; the zero is
+                // materialised here (the compiler spilled a hoisted constant
+                // zero pair and reloaded it from scratch on this path)
+                unsigned z;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                omx[0] = z;
+                omx[1] = z;
             }
         }
         __syncthreads();
