@@ -152,19 +152,48 @@ __global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs
         if (tx < tx0 || tx > tx1) mx = fmaxf(mx, tmax[tx]);
     // the ROI tiles: every load of a wave's (up to MT) tiles before the first
     // reduction -- one memory latency instead of one per tile
+    // (unconditional loads of clamped in-bounds pixels, masked after all of
+    // them: a masked spec_ld, widening fp16 where it loaded, waited for each
+    // of its loads in turn -- 20 memory round trips per wave)
+    auto pix = [&](int base, int i, int j, bool &ok) {  // pixel j of tile i: its index, ok = inside the ROI row
+        const int tx = base + i * NW, p = lane + 64 * j;
+        const int y = ty * kTile + (p >> 4), x = min(tx, tx1) * kTile + (p & 15);
+        ok = tx <= tx1 && y < L && x < L;
+        return ok ? (size_t)y * L + x : (size_t)0;
+    };
     for (int base = tx0 + w; base <= tx1; base += MT * NW) {
         float m[MT];
+        if (st.spec16) {  // uniform
+            const __half2 *sp = st.spec16 + (size_t)b * L * L;
+            __half2 hv[MT][4];
+            bool ok[MT][4];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
-            const int tx = base + i * NW;
-            m[i] = 0.f;
-            if (tx <= tx1) {  // wave-uniform
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) hv[i][j] = sp[pix(base, i, j, ok[i][j])];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                m[i] = 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int p = lane + 64 * j;
-                    const int y = ty * kTile + (p >> 4), x = tx * kTile + (p & 15);
-                    if (y < L && x < L) m[i] = fmaxf(m[i], cmag(spec_ld(st, b, (size_t)y * L + x)));
+                    const float2 f = __half22float2(hv[i][j]);
+                    const float a = cmag(make_float2(f.x * st.hinv, f.y * st.hinv));  // spec_ld's widening
+                    m[i] = fmaxf(m[i], ok[i][j] ? a : 0.f);
                 }
+            }
+        } else {
+            const float2 *sp = st.spec + (size_t)b * L * L;
+            float2 ov[MT][4];
+            bool ok[MT][4];
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ov[i][j] = sp[pix(base, i, j, ok[i][j])];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                m[i] = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m[i] = fmaxf(m[i], ok[i][j] ? cmag(ov[i][j]) : 0.f);
             }
         }
 #pragma unroll
@@ -1006,10 +1035,30 @@ __global__ void __launch_bounds__(NT) k_crop4k_cols1(DevState st, float2 *out, c
     const int sx = (x + L / 2) & (L - 1);
     const bool live = sx >= st.sx0 && sx <= st.sx1;
     float2 v[8];
+    // unconditional loads of clamped indices, masked after all eight (a
+    // masked spec_ld widens fp16 where it loads: one round trip per q)
+    bool ok[8];
+    size_t idx[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int sy = (n1 + 64 * (j + 8 * q) + L / 2) & (L - 1);
-        v[q] = live && sy >= st.sy0 && sy <= st.sy1 ? spec_ld(st, b, (size_t)sy * L + sx) : make_float2(0.f, 0.f);
+        ok[q] = live && sy >= st.sy0 && sy <= st.sy1;
+        idx[q] = (size_t)b * L * L + (ok[q] ? (size_t)sy * L + sx : 0);
+    }
+    if (st.spec16) {  // uniform
+        __half2 hv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) hv[q] = st.spec16[idx[q]];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float2 f = __half22float2(hv[q]);
+            v[q] = ok[q] ? make_float2(f.x * st.hinv, f.y * st.hinv) : make_float2(0.f, 0.f);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = st.spec[idx[q]];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = ok[q] ? v[q] : make_float2(0.f, 0.f);
     }
     idft64(v, lds, c, j, tw);
     float2 *o = out + (size_t)b * L * L + x;

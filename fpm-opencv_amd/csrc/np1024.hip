@@ -173,31 +173,55 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;         // + kx (:358-362)
     float2 x[16];
     float pmx = 0.f;
-    // every load of the row first, then the arithmetic and the pupil stores:
-    // a store to pup between the loads made the compiler keep them in program
-    // order (pup may alias the spectrum and dP), one memory latency per j
-    float2 pv[16], dv[16], ov[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int kx = fold(4 * (t + 16 * j) + c);
-        const bool in = kx * kx <= w2;
-        pv[j] = in ? pup[kx] : make_float2(0.f, 0.f);
-        dv[j] = (in && commit) ? dP[kx] : make_float2(0.f, 0.f);
-        ov[j] = in ? spec_ld(st, b, srow + kx) : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    // the row's loads half a row at a time, each half's loads all issued
+    // before its arithmetic and pupil stores (a store to pup between the loads
+    // made the compiler keep them in program order: pup may alias the
+    // spectrum and dP).  The loads are unconditional (a lane off the disk
+    // reads the row's centre pixel, in bounds, and its value is masked below)
+    // and the fp16 spectrum is widened after them: a masked spec_ld,
+    // converting where it loaded, waited for each of its loads in turn (16
+    // memory round trips per row); all sixteen at once spilled 22 VGPRs.
+    auto body = [&](int j, float2 p, float2 d, float2 o) {
         const int kx = fold(4 * (t + 16 * j) + c);
         x[j] = make_float2(0.f, 0.f);
         if (kx * kx <= w2) {
-            float2 p = pv[j];
             if (commit) {
-                p.x += dv[j].x / omax;
-                p.y += dv[j].y / omax;
+                p.x += d.x / omax;
+                p.y += d.y / omax;
                 pup[kx] = p;
             }
             pmx = fmaxf(pmx, cmag(p));
-            x[j] = cmul(ov[j], p);  // :364
+            x[j] = cmul(o, p);  // :364
+        }
+    };
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        float2 pv[8], dv[8];
+        int kc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int kx = fold(4 * (t + 16 * (8 * hh + i)) + c);
+            kc[i] = kx * kx <= w2 ? kx : 0;
+            pv[i] = pup[kc[i]];
+            dv[i] = dP[kc[i]];  // unconditional (used only when commit): a branch here waited for the load
+        }
+        if (st.spec16) {  // uniform
+            const __half2 *sp = st.spec16 + (size_t)b * st.L * st.L + srow;
+            __half2 hv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) hv[i] = sp[kc[i]];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float2 f = __half22float2(hv[i]);
+                body(8 * hh + i, pv[i], dv[i], make_float2(f.x * st.hinv, f.y * st.hinv));
+            }
+        } else {
+            const float2 *sp = st.spec + (size_t)b * st.L * st.L + srow;
+            float2 ov[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ov[i] = sp[kc[i]];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) body(8 * hh + i, pv[i], dv[i], ov[i]);
         }
     }
     pmx = wave_max(pmx);
@@ -347,12 +371,33 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
 #pragma unroll
     for (int hp = 0; hp < 2; ++hp) {
         float2 ov[8], pv[8];
+        // unconditional loads (off-disk lanes read the row's centre pixel,
+        // masked below), the fp16 spectrum widened after all of them (see R1)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int kx = fold(t + 16 * (4 * c + (i & 3)) + 256 * (2 * hp + (i >> 2)));
-            const bool in = kx * kx <= w2;
-            ov[i] = in ? spec_ld(st, b, srow + kx) : make_float2(0.f, 0.f);
-            pv[i] = in ? pup[kx] : make_float2(0.f, 0.f);
+            pv[i] = pup[kx * kx <= w2 ? kx : 0];
+        }
+        if (st.spec16) {  // uniform
+            const __half2 *sp = st.spec16 + (size_t)b * st.L * st.L + srow;
+            __half2 hv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int kx = fold(t + 16 * (4 * c + (i & 3)) + 256 * (2 * hp + (i >> 2)));
+                hv[i] = sp[kx * kx <= w2 ? kx : 0];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float2 f = __half22float2(hv[i]);
+                ov[i] = make_float2(f.x * st.hinv, f.y * st.hinv);
+            }
+        } else {
+            const float2 *sp = st.spec + (size_t)b * st.L * st.L + srow;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int kx = fold(t + 16 * (4 * c + (i & 3)) + 256 * (2 * hp + (i >> 2)));
+                ov[i] = sp[kx * kx <= w2 ? kx : 0];
+            }
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {

@@ -20,6 +20,10 @@ CASES = [  # (name, environment, geometry)
     ("dist_ks8", {"FPM_DIST": "8"}, G256),
     ("np90_s90", {}, (90, 360, 30, 5, 24)),       # k_fused_s90 (configs 1 / 2)
     ("np200_mr", {}, (200, 600, 26, 5, 40)),      # k_fused_mr (config 3)
+    # the general path's Np 1024 register kernels + K4 + the L 4096 objCrop
+    # passes (config 5 shape at L 2048 / 4096, fp16 spectrum storage: flag 2)
+    ("np1024_fp16", {"CMP_FLAGS": "2", "CMP_NPATCH": "1"}, (1024, 4096, 333, 3, 200)),
+    ("np1024_fp32", {"CMP_NPATCH": "2"}, (1024, 2048, 120, 3, 100)),
 ]
 
 CHILD = r"""
@@ -29,8 +33,10 @@ import fpm_amd
 from tools.synth import grid_geometry, make_stack
 Np, L, r, nside, step = (int(v) for v in sys.argv[2:7])
 x0, y0, order = grid_geometry(Np, L, nside, step)
-stack = make_stack(Np, L, r, x0, y0, n_patch=4, seed=7)
-prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=4)
+import os
+npatch = int(os.environ.get("CMP_NPATCH", "4"))
+stack = make_stack(Np, L, r, x0, y0, n_patch=npatch, seed=7)
+prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=npatch, flags=int(os.environ.get("CMP_FLAGS", "0")))
 out = fpm_amd.run_fpm(prob, stack, 2)
 np.savez(sys.argv[1], **{k: np.asarray(out[k]) for k in ("objF", "objCrop", "pupil")})
 """
