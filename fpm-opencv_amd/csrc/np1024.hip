@@ -137,9 +137,16 @@ __device__ __forceinline__ void w1k_ND(float2 (&x)[16], float2 *wt, const float2
 
 __device__ __forceinline__ int fold(int k) { return k < n1k::H ? k : k - n1k::N; }  // signed frequency
 
-// stage the N-point twiddle table; returns the table
+// stage the N-point twiddle table; returns the table (a thread's loads all
+// issued before its LDS stores: the rolled loop waited for each in turn)
+template <int NTB>
 __device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__restrict__ tw) {
-    for (int i = threadIdx.x; i < n1k::N; i += blockDim.x) sm[i] = tw[i];
+    static_assert(n1k::N % NTB == 0, "whole rounds");
+    float2 v[n1k::N / NTB];
+#pragma unroll
+    for (int i = 0; i < n1k::N / NTB; ++i) v[i] = tw[threadIdx.x + NTB * i];
+#pragma unroll
+    for (int i = 0; i < n1k::N / NTB; ++i) sm[threadIdx.x + NTB * i] = v[i];
     __syncthreads();
     return sm;
 }
@@ -157,7 +164,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     __shared__ float red[WPB];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const int lane = threadIdx.x & 63;
-    const float2 *twL = stage_twiddles(sm, tw);
+    const float2 *twL = stage_twiddles<NT>(sm, tw);
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
     float omax = 1.f;
@@ -257,7 +264,7 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
     constexpr int NTC = 64 * CW, SPCC = CW + 1;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
-    const float2 *twL = stage_twiddles(sm, tw);
+    const float2 *twL = stage_twiddles<NTC>(sm, tw);
     float2 *strip = sm + N;            // nb x SPCC (box rows only); the wave tiles
     float2 *wt = strip + w * WTILE;    // alias it while every column is in registers
     // XCD-aware column groups: the dispatcher deals blocks round-robin over the
@@ -269,14 +276,43 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
     __half2 *T16 = st.T16 ? st.T16 + (size_t)b * nb * N + x0 : nullptr;
     // FFT row i of a column is box row j = i + r (i <= r) or i - N + r
     // (i >= N - r) (:364: every other row is zero)
-    for (int idx = threadIdx.x; idx < nb * CW; idx += NTC) {
-        const int j = idx / CW, cc = idx - j * CW;
-        if (T16) {
-            const float2 h = __half22float2(T16[(size_t)j * N + cc]);
-            const float is = st.tsr[(size_t)b * nb + j];
-            strip[j * SPCC + cc] = make_float2(h.x * is, h.y * is);
+    // the box rows of the strip: a thread's loads all issued before its LDS
+    // stores (clamped indices, masked stores; the rolled loop waited for each
+    // load in turn, ~10 memory round trips per thread at config 5)
+    {
+        constexpr int KMAX = (N * CW + NTC - 1) / NTC;  // nb <= N rows
+        const int tot = nb * CW;
+        if (T16) {  // uniform
+            __half2 hv[KMAX];
+            float sv[KMAX];
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                const int idx = min((int)threadIdx.x + NTC * k, tot - 1), j = idx / CW, cc = idx - j * CW;
+                if (NTC * k < tot) {  // uniform
+                    hv[k] = T16[(size_t)j * N + cc];
+                    sv[k] = st.tsr[(size_t)b * nb + j];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                const int idx = (int)threadIdx.x + NTC * k, j = idx / CW, cc = idx - j * CW;
+                if (NTC * k < tot && idx < tot) {
+                    const float2 h = __half22float2(hv[k]);
+                    strip[j * SPCC + cc] = make_float2(h.x * sv[k], h.y * sv[k]);
+                }
+            }
         } else {
-            strip[j * SPCC + cc] = T[(size_t)j * N + cc];
+            float2 tv[KMAX];
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                const int idx = min((int)threadIdx.x + NTC * k, tot - 1), j = idx / CW, cc = idx - j * CW;
+                if (NTC * k < tot) tv[k] = T[(size_t)j * N + cc];
+            }
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                const int idx = (int)threadIdx.x + NTC * k, j = idx / CW, cc = idx - j * CW;
+                if (NTC * k < tot && idx < tot) strip[j * SPCC + cc] = tv[k];
+            }
         }
     }
     __syncthreads();
@@ -336,7 +372,7 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     __shared__ float red[WPB];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
-    const float2 *twL = stage_twiddles(sm, tw);
+    const float2 *twL = stage_twiddles<NT>(sm, tw);
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
     // max|P| of the previous commit from its npart partial maxima (:415)
