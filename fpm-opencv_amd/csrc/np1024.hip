@@ -375,26 +375,47 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     const float2 *twL = stage_twiddles<NT>(sm, tw);
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
-    // max|P| of the previous commit from its npart partial maxima (:415)
-    float pm = 0.f;
-    for (int i = threadIdx.x; i < st.npart; i += NT) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
-    pm = block_max(pm, red);
-    if (row >= nb) return;
-    const int ky = row - r, w2 = r * r - ky * ky;
+    // the row's T first (its memory latency runs under the max|P| reduction
+    // below), then max|P| of the previous commit from its npart partial
+    // maxima (:415) -- every load of both issued before the first use (the
+    // rolled partial loop waited for each load in turn)
+    const int rowc = row < nb ? row : nb - 1;  // rows past the box: in-bounds loads, discarded
     float2 x[16];
-    if (st.T16) {  // column j's element times its column scale
-        const __half2 *Tr = st.T16 + ((size_t)b * nb + row) * N + c;
+    __half2 hT[16];
+    float sT[16];
+    if (st.T16) {  // uniform
+        const __half2 *Tr = st.T16 + ((size_t)b * nb + rowc) * N + c;
         const float *is = st.tsc + (size_t)b * N + c;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const float2 h = __half22float2(Tr[4 * (t + 16 * j)]);
-            const float s = is[4 * (t + 16 * j)];
-            x[j] = make_float2(h.x * s, h.y * s);
+            hT[j] = Tr[4 * (t + 16 * j)];
+            sT[j] = is[4 * (t + 16 * j)];
         }
     } else {
-        const float2 *Tr = st.T + ((size_t)b * nb + row) * N + c;
+        const float2 *Tr = st.T + ((size_t)b * nb + rowc) * N + c;
 #pragma unroll
         for (int j = 0; j < 16; ++j) x[j] = Tr[4 * (t + 16 * j)];
+    }
+    constexpr int KP = (N + NT - 1) / NT;  // npart = nb <= N partials
+    float pv4[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const int i = threadIdx.x + NT * k;
+        pv4[k] = st.pmax[b * st.npart + (i < st.npart ? i : 0)];
+    }
+    float pm = 0.f;
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+        if ((int)threadIdx.x + NT * k < st.npart) pm = fmaxf(pm, pv4[k]);
+    pm = block_max(pm, red);
+    if (row >= nb) return;
+    const int ky = row - r, w2 = r * r - ky * ky;
+    if (st.T16) {  // column j's element times its column scale
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float2 h = __half22float2(hT[j]);
+            x[j] = make_float2(h.x * sT[j], h.y * sT[j]);
+        }
     }
     w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (rows)
     float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
