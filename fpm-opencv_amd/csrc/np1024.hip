@@ -137,20 +137,6 @@ __device__ __forceinline__ void w1k_ND(float2 (&x)[16], float2 *wt, const float2
 
 __device__ __forceinline__ int fold(int k) { return k < n1k::H ? k : k - n1k::N; }  // signed frequency
 
-// stage the N-point twiddle table; returns the table (a thread's loads all
-// issued before its LDS stores: the rolled loop waited for each in turn)
-template <int NTB>
-__device__ __forceinline__ float2 *stage_twiddles(float2 *sm, const float2 *__restrict__ tw) {
-    static_assert(n1k::N % NTB == 0, "whole rounds");
-    float2 v[n1k::N / NTB];
-#pragma unroll
-    for (int i = 0; i < n1k::N / NTB; ++i) v[i] = tw[threadIdx.x + NTB * i];
-#pragma unroll
-    for (int i = 0; i < n1k::N / NTB; ++i) sm[threadIdx.x + NTB * i] = v[i];
-    __syncthreads();
-    return sm;
-}
-
 // R1: grid (ceil(nb / WPB), B), block NT.  Also the previous LED's pupil
 // commit (general.hip K5, folded in when `commit`): P += dP / max|objF| on
 // this row's disk pixels (:468-475), with max|objF| from the tile-row maxima
@@ -164,30 +150,77 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     __shared__ float red[WPB];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const int lane = threadIdx.x & 63;
-    const float2 *twL = stage_twiddles<NT>(sm, tw);
-    float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
-    float omax = 1.f;
-    if (commit) {  // block-uniform
-        float m = 0.f;
-        for (int i = threadIdx.x; i < st.nty; i += NT) m = fmaxf(m, st.rmax[(size_t)b * st.nty + i]);
-        omax = block_max(m, red);
+    // the twiddle table's loads, max|objF| of the previous LED from K4's
+    // tile-row maxima, then the first half row's loads, all issued before the
+    // twiddle stores and the reduction's barriers: their memory latencies
+    // overlap instead of following each other (loads unconditional: a branch
+    // on `commit` waited for its load)
+    static_assert(N % NT == 0, "whole rounds");
+    float2 twv[N / NT];
+#pragma unroll
+    for (int i = 0; i < N / NT; ++i) twv[i] = tw[threadIdx.x + NT * i];
+    const float2 *twL = sm;
+    float2 *wt = sm + N + w * WTILE;
+    float rm[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = threadIdx.x + NT * k;
+        rm[k] = st.rmax[(size_t)b * st.nty + (i < st.nty ? i : 0)];
     }
-    if (row >= nb) return;  // wave-uniform; no block barrier follows
-    const int ky = row - r, w2 = r * r - ky * ky;
-    float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;         // indexed by kx
-    const float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
+    const int rowc = row < nb ? row : nb - 1;  // rows past the box: in-bounds loads, discarded
+    const int ky = rowc - r, w2 = r * r - ky * ky;
+    float2 *pup = st.pupil + ((size_t)b * nb + rowc) * nb + r;        // indexed by kx
+    const float2 *dP = st.dP + ((size_t)b * nb + rowc) * nb + r;
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;         // + kx (:358-362)
     float2 x[16];
     float pmx = 0.f;
-    // the row's loads half a row at a time, each half's loads all issued
+    // The row's loads half a row at a time, each half's loads all issued
     // before its arithmetic and pupil stores (a store to pup between the loads
     // made the compiler keep them in program order: pup may alias the
     // spectrum and dP).  The loads are unconditional (a lane off the disk
-    // reads the row's centre pixel, in bounds, and its value is masked below)
-    // and the fp16 spectrum is widened after them: a masked spec_ld,
-    // converting where it loaded, waited for each of its loads in turn (16
-    // memory round trips per row); all sixteen at once spilled 22 VGPRs.
+    // reads the row's centre pixel, in bounds, and its value is masked) and
+    // the fp16 spectrum is widened after them: a masked spec_ld, converting
+    // where it loaded, waited for each of its loads in turn (16 memory round
+    // trips per row); all sixteen at once spilled 22 VGPRs.
+    struct Half {
+        float2 pv[8], dv[8], ov[8];
+        __half2 hv[8];
+        int kc[8];
+    };
+    auto load_half = [&](int hh, Half &q) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int kx = fold(4 * (t + 16 * (8 * hh + i)) + c);
+            q.kc[i] = kx * kx <= w2 ? kx : 0;
+            q.pv[i] = pup[q.kc[i]];
+            q.dv[i] = dP[q.kc[i]];  // unconditional (used only when commit): a branch here waited for the load
+        }
+        if (st.spec16) {  // uniform
+            const __half2 *sp = st.spec16 + (size_t)b * st.L * st.L + srow;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) q.hv[i] = sp[q.kc[i]];
+        } else {
+            const float2 *sp = st.spec + (size_t)b * st.L * st.L + srow;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) q.ov[i] = sp[q.kc[i]];
+        }
+    };
+    Half q;
+    load_half(0, q);
+#pragma unroll
+    for (int i = 0; i < N / NT; ++i) sm[threadIdx.x + NT * i] = twv[i];
+    if (!commit) __syncthreads();  // block-uniform; else block_max's barriers order the stores
+    float omax = 1.f;
+    if (commit) {  // block-uniform
+        float m = 0.f;
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if ((int)threadIdx.x + NT * k < st.nty) m = fmaxf(m, rm[k]);
+        for (int i = threadIdx.x + 2 * NT; i < st.nty; i += NT) m = fmaxf(m, st.rmax[(size_t)b * st.nty + i]);  // L > 8192 only
+        omax = block_max(m, red);
+    }
+    if (row >= nb) return;  // wave-uniform; no block barrier follows
     auto body = [&](int j, float2 p, float2 d, float2 o) {
         const int kx = fold(4 * (t + 16 * j) + c);
         x[j] = make_float2(0.f, 0.f);
@@ -203,32 +236,16 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     };
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-        float2 pv[8], dv[8];
-        int kc[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int kx = fold(4 * (t + 16 * (8 * hh + i)) + c);
-            kc[i] = kx * kx <= w2 ? kx : 0;
-            pv[i] = pup[kc[i]];
-            dv[i] = dP[kc[i]];  // unconditional (used only when commit): a branch here waited for the load
-        }
+        if (hh == 1) load_half(1, q);  // behind the first half's pupil stores
         if (st.spec16) {  // uniform
-            const __half2 *sp = st.spec16 + (size_t)b * st.L * st.L + srow;
-            __half2 hv[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) hv[i] = sp[kc[i]];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const float2 f = __half22float2(hv[i]);
-                body(8 * hh + i, pv[i], dv[i], make_float2(f.x * st.hinv, f.y * st.hinv));
+                const float2 f = __half22float2(q.hv[i]);
+                body(8 * hh + i, q.pv[i], q.dv[i], make_float2(f.x * st.hinv, f.y * st.hinv));
             }
         } else {
-            const float2 *sp = st.spec + (size_t)b * st.L * st.L + srow;
-            float2 ov[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) ov[i] = sp[kc[i]];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) body(8 * hh + i, pv[i], dv[i], ov[i]);
+            for (int i = 0; i < 8; ++i) body(8 * hh + i, q.pv[i], q.dv[i], q.ov[i]);
         }
     }
     pmx = wave_max(pmx);
@@ -264,7 +281,14 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
     constexpr int NTC = 64 * CW, SPCC = CW + 1;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
-    const float2 *twL = stage_twiddles<NTC>(sm, tw);
+    // the twiddle table and the strip staged together, under one barrier: a
+    // thread's twiddle loads, then its strip loads, all issued before any LDS
+    // store (the twiddles' own barrier kept the strip's loads behind it)
+    static_assert(N % NTC == 0, "whole rounds");
+    float2 twv[N / NTC];
+#pragma unroll
+    for (int i = 0; i < N / NTC; ++i) twv[i] = tw[threadIdx.x + NTC * i];
+    const float2 *twL = sm;
     float2 *strip = sm + N;            // nb x SPCC (box rows only); the wave tiles
     float2 *wt = strip + w * WTILE;    // alias it while every column is in registers
     // XCD-aware column groups: the dispatcher deals blocks round-robin over the
@@ -282,6 +306,10 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
     {
         constexpr int KMAX = (N * CW + NTC - 1) / NTC;  // nb <= N rows
         const int tot = nb * CW;
+        auto store_tw = [&]() {
+#pragma unroll
+            for (int i = 0; i < N / NTC; ++i) sm[threadIdx.x + NTC * i] = twv[i];
+        };
         if (T16) {  // uniform
             __half2 hv[KMAX];
             float sv[KMAX];
@@ -293,6 +321,7 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
                     sv[k] = st.tsr[(size_t)b * nb + j];
                 }
             }
+            store_tw();
 #pragma unroll
             for (int k = 0; k < KMAX; ++k) {
                 const int idx = (int)threadIdx.x + NTC * k, j = idx / CW, cc = idx - j * CW;
@@ -308,6 +337,7 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
                 const int idx = min((int)threadIdx.x + NTC * k, tot - 1), j = idx / CW, cc = idx - j * CW;
                 if (NTC * k < tot) tv[k] = T[(size_t)j * N + cc];
             }
+            store_tw();
 #pragma unroll
             for (int k = 0; k < KMAX; ++k) {
                 const int idx = (int)threadIdx.x + NTC * k, j = idx / CW, cc = idx - j * CW;
@@ -372,7 +402,11 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     __shared__ float red[WPB];
     const int w = threadIdx.x >> 6, c = (threadIdx.x >> 4) & 3, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
-    const float2 *twL = stage_twiddles<NT>(sm, tw);
+    static_assert(N % NT == 0, "whole rounds");
+    float2 twv[N / NT];  // the twiddle table: loads first, stored before block_max's barriers
+#pragma unroll
+    for (int i = 0; i < N / NT; ++i) twv[i] = tw[threadIdx.x + NT * i];
+    const float2 *twL = sm;
     float2 *wt = sm + N + w * WTILE;
     const int r = st.r, nb = st.nb, b = blockIdx.y, row = blockIdx.x * WPB + w;
     // the row's T first (its memory latency runs under the max|P| reduction
@@ -407,6 +441,8 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
 #pragma unroll
     for (int k = 0; k < KP; ++k)
         if ((int)threadIdx.x + NT * k < st.npart) pm = fmaxf(pm, pv4[k]);
+#pragma unroll
+    for (int i = 0; i < N / NT; ++i) sm[threadIdx.x + NT * i] = twv[i];
     pm = block_max(pm, red);
     if (row >= nb) return;
     const int ky = row - r, w2 = r * r - ky * ky;
