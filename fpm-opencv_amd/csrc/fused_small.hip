@@ -314,12 +314,20 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;  // wave-uniform
                 const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
                 float mm = 0.f;
+                // the tile's four loads issued together (clamped in bounds, masked
+                // after): a conditional load waited for each in turn
+                float2 e[4];
+                bool ok[4];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int pp = lane + 64 * jj;
                     const int yy = ty * 16 + (pp >> 4), xx = tx * 16 + (pp & 15);
-                    if (yy < L && xx < L) mm = fmaxf(mm, cmag(spec[(unsigned)(yy * L + xx)]));
+                    ok[jj] = yy < L && xx < L;
+                    e[jj] = spec[ok[jj] ? (unsigned)(yy * L + xx) : 0u];
                 }
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    if (ok[jj]) mm = fmaxf(mm, cmag(e[jj]));
                 mm = wave_max(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
