@@ -664,12 +664,15 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             for (int k = w; k < a.nbt; k += NW) {
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u) || !(tmx[k] > cm)) continue;  // wave-uniform
                 const int ty = a.bty0 + band_dy(k), tx = a.btx0 + k - band_dy(k) * a.nbx;
-                float mm = 0.f;
+                float2 e[4];  // all four loads before the first use (else one round trip each)
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int pp = lane + 64 * jj;
-                    mm = fmaxf(mm, cmag(spec[(unsigned)((ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15))]));
+                    e[jj] = spec[(unsigned)((ty * 16 + (pp >> 4)) * L + tx * 16 + (pp & 15))];
                 }
+                float mm = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) mm = fmaxf(mm, cmag(e[jj]));
                 mm = wave_max(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
