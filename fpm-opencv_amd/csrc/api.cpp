@@ -63,12 +63,6 @@ int fused_split_parts(int nt, int B, int n_cu);
 // distributed mode of the Np 256 kernel (fused_dist.hip)
 size_t fused_dist_elems(int B, int ks);
 int fused_dist_parts(int B, int n_cu, int r, int L);
-// Np 90 distributed over 2 / 4 workgroups per patch (fused_s90d.hip)
-int fused_s90d_parts(int B, int n_cu);
-size_t fused_s90d_elems(int B, int ks);
-hipError_t launch_fused_s90d(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
-                             const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, int stall_led, hipStream_t s);
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
                              float2 *area, int *flags, int stall_led, hipStream_t s);
@@ -191,7 +185,6 @@ struct fpm_ctx {
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
-    bool s90d = false;              // ... distributed over split_ks workgroups per patch (fused_s90d.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -469,13 +462,9 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         // workgroup per patch
         const int dks = c->fused_nt ? fused_dist_parts(B, n_cu, r, L) : 0;
         c->dist = dks > 1;
-        const int sks = c->fused_s90 ? fused_s90d_parts(B, n_cu) : 0;
-        c->s90d = sks > 1;
-        c->split_ks = c->dist ? dks : c->s90d ? sks : c->fused_nt ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
+        c->split_ks = c->dist ? dks : c->fused_nt ? fused_split_parts(c->fused_nt, B, n_cu) : 1;
         if (c->split_ks > 1) {
-            const size_t nx = c->dist   ? fused_dist_elems(B, c->split_ks)
-                              : c->s90d ? fused_s90d_elems(B, c->split_ks)
-                                        : fused_xch_elems(B, c->split_ks);
+            const size_t nx = c->dist ? fused_dist_elems(B, c->split_ks) : fused_xch_elems(B, c->split_ks);
             if ((rc = dalloc(c, &c->xch, nx))) return fail(rc);
             const size_t nf = fused_flag_words(B, c->split_ks);
             if ((rc = dalloc(c, &c->split_flags, nf))) return fail(rc);
@@ -747,10 +736,7 @@ int fpm_run(fpm_ctx *c, int iters) {
     HIP_TRY(hipEventRecord(ev[0], c->stream));
     for (int it = 0; it < iters; ++it) {
         HIP_TRY(hipEventRecord(ev[1 + 3 * it], c->stream));
-        if (c->path == FPM_PATH_FUSED && c->s90d) {
-            HIP_TRY(launch_fused_s90d(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev, c->prob.n_order, c->tw_np,
-                                      c->split_ks, c->dbg, c->xch, c->split_flags, c->stall_led, c->stream));
-        } else if (c->path == FPM_PATH_FUSED && c->fused_s90) {
+        if (c->path == FPM_PATH_FUSED && c->fused_s90) {
             HIP_TRY(launch_fused_s90_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                                c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED && c->fused_small) {
@@ -820,7 +806,7 @@ int fpm_run(fpm_ctx *c, int iters) {
                                         "split:Fstores", "split:Fwait"};
         const char *names_d[kStamps] = {"gather", "A", "sync1", "B", "sync2", "C", "update", "sync3",
                                         "merge+Opre", "max", "P", "C:rows(sub)", "sync3:acks(sub)"};
-        const char *const *names = c->dist || c->s90d ? names_d : names_f;
+        const char *const *names = c->dist ? names_d : names_f;
         for (int v = 0; v < 2; ++v) {
             fprintf(stderr, "[fpm stamps] cycles per LED step (%s wave view, mean over blocks):", v ? "last" : "first");
             for (int i = 0; i < kStamps; ++i) fprintf(stderr, " %s=%.0f", names[i], h[v * kStamps + i] / steps);
@@ -926,7 +912,6 @@ static void fill_info(const fpm_ctx *c, fpm_info *info) {
                          : c->dist             ? FPM_KERNEL_FUSED_NP256_DIST
                                                : FPM_KERNEL_FUSED_NP256;
     info->threads_per_wg = c->path != FPM_PATH_FUSED ? 0
-                           : c->s90d ? (c->split_ks == 2 ? 512 : 256)
                            : c->fused_s90 || c->fused_small ? 1024
                            : c->fused_mr ? 768
                                          : c->fused_nt;
