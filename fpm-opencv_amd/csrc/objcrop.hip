@@ -292,8 +292,11 @@ __global__ void __launch_bounds__(64 * W) k_crop_rows600(const float2 *__restric
 // columns per thread); the loads of piece h + 2 are issued as soon as piece h
 // has left its registers, so two pieces are in flight while the block works
 // (round 3's version loaded piece by piece with 8-byte loads: 2.4 TB/s, SQ
-// wait_any 0.65 of wave cycles).  W 4 / NH 4: 24-column strips (192-byte row
-// segments, 64-byte aligned), 30 KB pieces.
+// wait_any 0.65 of wave cycles).  W 4 / NH 2: 24-column strips (192-byte row
+// segments, 64-byte aligned), 59 KB pieces, both pieces' loads in flight from
+// the start (round 5: NH 4 -> 2 took config 3's objCrop from 0.448 to 0.345
+// ms per step; NH 1, a 600-row strip and one block per CU, 0.45 ms;
+// profiles/r05_ab/crop600_pieces_ab.txt).
 // grid (ceil(L / G), B), block 64 W
 template <int W, int NH>
 __global__ void __launch_bounds__(64 * W) k_crop_cols600(float2 *__restrict__ io, const float2 *__restrict__ tw_L,
@@ -581,7 +584,9 @@ hipError_t launch_objcrop_regs(const DevState &st, float2 *out, const float2 *tw
         case 512: return launch_crop<2, kCropGR, kCropG>(st, out, tw_L, s);
         case 768: return launch_crop<3, kCropGR, kCropG>(st, out, tw_L, s);
         case 1024: return launch_crop<4, kCropGR, kCropG>(st, out, tw_L, s);
-        case 600: return c600::launch_crop600<1, 4, 4>(st, out, tw_L, s);
+        // L 600: row pass 12 rows per block (2 waves; 6 rows: 0.345 -> 0.336 ms
+        // per step), column pass 24-column strips in two pieces
+        case 600: return c600::launch_crop600<2, 4, 2>(st, out, tw_L, s);
         case 360: return c360::launch_crop360<1, 4>(st, out, tw_L, s);
         default: return hipErrorNotSupported;
     }

@@ -58,7 +58,12 @@ def main():
             za, zb = np.load(pa), np.load(pb)
             same = all(np.array_equal(za[k], zb[k]) for k in za.files)
             ok = ok and same
-            print(f"{name}: {'bit-identical' if same else 'DIFFERENT'}")
+            if same:
+                print(f"{name}: bit-identical")
+            else:  # which outputs moved, by how much (relative L2)
+                rel = {k: float(np.linalg.norm(za[k] - zb[k]) / max(np.linalg.norm(za[k]), 1e-30))
+                       for k in za.files if not np.array_equal(za[k], zb[k])}
+                print(f"{name}: DIFFERENT " + " ".join(f"{k} rel {v:.2e}" for k, v in rel.items()))
     sys.exit(0 if ok else 1)
 
 
