@@ -15,9 +15,9 @@ fi
 if [ -z "$NO_CMP" ]; then
 timeout -k 10 600 python tools/gpu/cmp_libs.py fpm-opencv_amd/lib/libfpm_hip.so fpm-opencv_amd/lib_$BASE/libfpm_hip.so > $O/cmp.txt 2>&1; rc=$?; cat $O/cmp.txt | tail -8; [ $rc -le 1 ] || exit 1
 fi
-args() { case $1 in metric) echo "";; pt128|pt128d2) echo "--patches-total 128";; pt64) echo "--patches-total 64";; pt32) echo "--patches-total 32";; c2|c2d2|c2d4) echo "--config c2";; c3) echo "--config c3";; c5) echo "--config c5";; esac; }
+args() { case $1 in metric) echo "";; pt128|pt128d2) echo "--patches-total 128";; pt64) echo "--patches-total 64";; pt32) echo "--patches-total 32";; c2) echo "--config c2";; c3) echo "--config c3";; c5) echo "--config c5";; esac; }
 # workload-specific environment (pt128d2: the 128-patch shard on the distributed kernel at 2 parts)
-wenv() { case $1 in pt128d2) echo "FPM_DIST=2";; c2d2) echo "FPM_S90D=2";; c2d4) echo "FPM_S90D=4";; *) echo "FPM_X=0";; esac; }
+wenv() { case $1 in pt128d2) echo "FPM_DIST=2";; *) echo "FPM_X=0";; esac; }
 for w in ${STAMPS:-}; do
   for V in ${STLIBS:-new $BASE}; do
     if [ $V = new ]; then unset FPM_HIP_LIB; else export FPM_HIP_LIB=$GRAFT_REPO_ROOT/fpm-opencv_amd/lib_$V/libfpm_hip.so; fi
