@@ -23,6 +23,14 @@ def src_hash(csrc: str = CSRC) -> str:
         h.update(name.encode())
         with open(p, "rb") as f:
             h.update(f.read())
+    # the compile flags decide the machine code too (round 5: the scheduler
+    # strategy); the HIPFLAGS line of the Makefile is part of the stamp
+    mk = os.path.join(os.path.dirname(csrc), "Makefile")
+    if os.path.isfile(mk):
+        with open(mk, "rb") as f:
+            for line in f.read().split(b"\n"):
+                if b"HIPFLAGS" in line or b"amdgpu-" in line:
+                    h.update(line)
     return h.hexdigest()[:16]
 
 
