@@ -35,6 +35,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "fpm-opencv_amd", "python"), os.path.jo
 METRIC = "LED-updates/sec (patch·LED/s), 256² patch × 293 LEDs; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 F32_PEAK_TFLOPS = 157.3    # FP32 vector == FP32 MFMA dense peak (MI355X_MICROARCH.md)
+F32_FLOPS_PER_CYCLE = 1024 * 64  # 256 CUs x 4 SIMDs x 64 f32 flops per cycle: the peak at any clock
 
 DOG_KEYS = {"cropSizeX": 256, "pixelSize": 6.5, "objectiveMag": 8.1485, "objectiveNA": 0.1,
             "maxIlluminationNA": 0.6, "lambda": 0.6292, "delta1": 10, "delta2": 3,
@@ -62,6 +63,8 @@ WORKLOADS = {
           "one runFPM iteration per step",
     "c2": "config 2: dataset_mono.json with the dome fallback (Np=90, L=360, naRadius 30, 193 LEDs), "
           "64 patches, one runFPM iteration per step",
+    "c2np256": "config 2 geometry at Np=256: dataset_mono.json with the dome fallback, cropSizeX 256 (L=1024, "
+               "naRadius 84, 193 LEDs; general path), 64 patches, one runFPM iteration per step",
 }
 
 
@@ -84,7 +87,7 @@ def config_geometry(name, np_=256):
         return metric_geometry(200, max_na=0.4)
     if name == "c2":
         import numpy as np
-        g = config1_geometry()
+        g = config1_geometry(np_)
         g["order_leds"] = np.arange(g["n_led"])
         return g
     if name == "c5":
@@ -184,7 +187,7 @@ def fp32_roof_updates_per_s(np_, nb, support_px):
     return F32_PEAK_TFLOPS * 1e12 / algorithmic_flops_per_update(np_, nb, support_px)
 
 
-def roofline_line(geo, info, per_launch_ms, per_launch_updates, pmc_path):
+def roofline_line(geo, info, per_launch_ms, per_launch_updates, pmc_path, clock=None):
     """roofline object of the bench line for the context's LED-update kernel.
 
     The fused kernels keep T in LDS and P in registers: they move the
@@ -206,6 +209,22 @@ def roofline_line(geo, info, per_launch_ms, per_launch_updates, pmc_path):
     sup_bytes = (2.0 * np_ * np_ + 32.0 * S) * per_launch_updates
     dense_bytes = dense_bytes_per_update(np_) * per_launch_updates
     roof_u = fp32_roof_updates_per_s(np_, info.box, S)
+    # the counters' FP32 view: SQ_INSTS_VALU_*_F32 count a packed
+    # instruction once, so the counted flops are a lower bound of the executed
+    # ones and twice them an upper bound; the 5 N log2 N model (frac above)
+    # exceeds even that upper bound (radix-16 transforms need fewer operations)
+    cyc = clock["kernel_cycles_per_launch"] if clock and clock.get("kernel_cycles_per_launch") else None
+    fl_cnt = counters.get("fp32_flops") if counters else None
+    counted = None
+    if fl_cnt:
+        counted = dict(
+            fp32_frac_counted=round(fl_cnt / t / 1e12 / F32_PEAK_TFLOPS, 4),
+            fp32_frac_counted_packed_upper=round(2 * fl_cnt / t / 1e12 / F32_PEAK_TFLOPS, 4),
+            counted_flops_per_launch=fl_cnt, model_over_packed_upper=round(flops / (2 * fl_cnt), 3),
+            note="SQ_INSTS_VALU_*_F32 count a v_pk_* instruction once: counted flops bound the executed ones "
+                 "from below, 2x counted from above; fractions of the 157.3 TF peak at the measured launch time")
+        if cyc:
+            counted["fp32_frac_counted_per_cycle"] = round(fl_cnt / (cyc * F32_FLOPS_PER_CYCLE), 4)
     hbm = dict(achieved=round(min_bytes / t / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                frac=round(min_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
                bytes_model=f"2*Np^2 (uint16 I) + 16*|S| (O read+write on the {S}-px support) per LED-update "
@@ -218,7 +237,12 @@ def roofline_line(geo, info, per_launch_ms, per_launch_updates, pmc_path):
                measured_GBs=(round(traffic / t / 1e9, 1) if traffic else None),
                traffic_over_algorithmic=(round(traffic / min_bytes, 3) if traffic else None))
     return dict(bound="valu", achieved=round(achieved_tf, 2), peak=F32_PEAK_TFLOPS, unit="TFLOP/s",
-                frac=round(achieved_tf / F32_PEAK_TFLOPS, 4), traffic=traffic,
+                frac=round(achieved_tf / F32_PEAK_TFLOPS, 4),
+                fp32_frac_counted=counted["fp32_frac_counted"] if counted else None,
+                frac_per_cycle=(round(flops / (cyc * F32_FLOPS_PER_CYCLE), 4) if cyc else None),
+                frac_per_cycle_note="model flops / (in-kernel cycles per launch x 65536 f32 flops per cycle): "
+                                    "the fraction independent of the box's clock",
+                fp32_counted=counted, traffic=traffic,
                 kernel=kname, launch_ms=round(per_launch_ms, 4),
                 flops_model=f"5 N log2 N per executed pruned 1-D DFT (nb={info.box} row IDFTs + Np column "
                             f"IDFT/DFT pairs + nb row DFTs) + 12 flop/px amplitude + 60 flop per support px, "
@@ -260,12 +284,15 @@ def host_cores():
     return cores, f"nproc {os.cpu_count()}, affinity {n_aff}, cgroup quota {quota or 'none'}"
 
 
-def config1_geometry():
+def config1_geometry(np_=90):
     """BASELINE configs[0]: dataset_mono.json with the 508-LED dome fallback
     (geometry and order from the reference's own jsoncpp probe,
-    tests/golden/geometry_mono_dome.json): Np 90, L 360, r 30, 193 LEDs."""
+    tests/golden/geometry_mono_dome.json): Np 90, L 360, r 30, 193 LEDs;
+    np_=256: the same dataset at cropSizeX 256 (geometry_mono_dome_np256.json:
+    L 1024, r 84, 193 LEDs)."""
     import numpy as np
-    with open(os.path.join(ROOT, "tests", "golden", "geometry_mono_dome.json")) as f:
+    fx = {90: "geometry_mono_dome.json", 256: "geometry_mono_dome_np256.json"}[np_]
+    with open(os.path.join(ROOT, "tests", "golden", fx)) as f:
         p = json.load(f)["probe"]
     leds = {l["led"]: l for l in p["leds"]}
     order = p["sorted_indices"]
@@ -323,7 +350,9 @@ def main():
                          "gathered and stitched on rank 0 after the timed region (0: north_star's 256-patch field "
                          "for --config metric, weak scaling for the other configs)")
     ap.add_argument("--weak", action="store_true", help="weak scaling: every rank owns --patches patches")
-    ap.add_argument("--np", type=int, default=256)
+    ap.add_argument("--np", type=int, default=0,
+                    help="patch size: 256 for --config metric (other Np: dogStomach optics at that size), "
+                         "90 for c2 (256: the same dataset at cropSizeX 256, naRadius 84, general path)")
     ap.add_argument("--config", default="metric", choices=["metric", "c2", "c3", "c5"],
                     help="workload (config_geometry); only 'metric' is the headline line")
     ap.add_argument("--fp16", action="store_true", help="fp16 spectrum storage (default for --config c5)")
@@ -380,6 +409,8 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if not args.np:
+        args.np = 90 if args.config == "c2" else 256
     geo = config_geometry(args.config, args.np)
     fp16 = args.fp16 or args.config == "c5"
     if args.patches_total <= 0 and not args.weak and args.config == "metric":
@@ -433,12 +464,18 @@ def main():
     led_ms = 0.0
     launches = 0
     crop_ms = 0.0
+    clk_cyc = clk_ms = 0.0
+    clk_n = 0
     for _ in range(args.steps):
         solver.run(1)
         t = solver.timing()
         led_ms += t.led_ms
         launches += t.led_launches
         crop_ms += t.objcrop_ms
+        k = solver.clock()  # block 0's s_memtime / s_memrealtime over the launch (fused path)
+        clk_cyc += k.cycles_per_launch * k.launches
+        clk_ms += k.ms_per_launch * k.launches
+        clk_n += k.launches
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -453,7 +490,15 @@ def main():
     per_launch_ms = led_ms / max(launches, 1)
     fused = info.path == fpm_amd.PATH_FUSED
     per_launch_updates = B * geo["n_led"] if fused else B
-    roofline = roofline_line(geo, info, per_launch_ms, per_launch_updates, args.pmc or default_pmc(args, info))
+    clock = None
+    if clk_n:
+        clock = dict(clock_mhz=round(clk_cyc / (clk_ms * 1e-3) / 1e6, 1),
+                     kernel_cycles_per_launch=round(clk_cyc / clk_n, 0),
+                     probe_ms_per_launch=round(clk_ms / clk_n, 4), launches=clk_n,
+                     note="block 0 of each LED-update launch: s_memtime (shader cycles) and s_memrealtime "
+                          "(100 MHz) at entry and after its last LED; a slow box reads as a lower clock at the "
+                          "same cycles (fpm_get_clock)")
+    roofline = roofline_line(geo, info, per_launch_ms, per_launch_updates, args.pmc or default_pmc(args, info), clock)
 
     gather = None
     if world > 1 and not args.no_gather:
@@ -532,8 +577,9 @@ def main():
             "dtype": "f32 (fp16 spectrum storage)" if fp16 else "f32",
             "data": ("synthetic: seeded FPM forward model (HR object, defocus pupil, Poisson noise), uint16"
                      if args.data == "model" else "random uint16 (profiling only)"),
-            "config": {"workload": WORKLOADS[args.config] if args.np == 256 or args.config != "metric" else
-                                   f"dogStomach optics, Np={geo['np_']}, one runFPM iteration per step",
+            "config": {"workload": (WORKLOADS["c2np256"] if args.config == "c2" and args.np == 256 else
+                                    WORKLOADS[args.config] if args.config != "metric" or args.np == 256 else
+                                    f"dogStomach optics, Np={geo['np_']}, one runFPM iteration per step"),
                        "patches_per_gpu": B, "leds": int(geo["n_led"]), "np": int(geo["np_"]),
                        "patches_total": int(args.patches_total if strong else B * world),
                        "scaling_mode": (f"strong: one {args.patches_total}-patch field sharded over {world} rank(s)"
@@ -543,6 +589,9 @@ def main():
                        "kernel": kernel_name(info), "workgroups_per_patch": int(info.wg_per_patch),
                        "parallelism": f"patch-sharded x{world}"},
             "roofline": roofline,
+            "clock_mhz": clock["clock_mhz"] if clock else None,
+            "kernel_cycles_per_launch": clock["kernel_cycles_per_launch"] if clock else None,
+            "clock": clock,
             "cpu_baseline": cpu,
             "setup": setup,
             "led_ms_per_step": round(led_ms / args.steps, 3),

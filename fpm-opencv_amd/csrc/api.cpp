@@ -80,8 +80,12 @@ size_t fused_T_elems(int np, int r, int B);
 // occupancy check, then a plain launch ordered after the previous co-resident
 // grid of this process on the same device (another context, another stream),
 // so two grids that each need every block resident never share the device.
-// Under stream capture the order is the capturing caller's business (an event
-// recorded outside the capture cannot be waited on inside it).
+// A capturing stream is refused (hipErrorStreamCaptureUnsupported): an event
+// recorded outside the capture cannot be waited on inside it, so a replayed
+// graph would carry no such order (fpm_run refuses capture before this).
+// Only co-resident grids are ordered against each other; other kernels on
+// other streams may still hold CUs, and then the waits' ~1 s timeout reports
+// the launch.
 hipError_t launch_coresident_raw(const void *fn, int grid, int block, size_t lds, void **args, hipStream_t s) {
     int dev = 0, n_cu = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -91,7 +95,7 @@ hipError_t launch_coresident_raw(const void *fn, int grid, int block, size_t lds
     if ((long long)per_cu * n_cu < grid) return hipErrorCooperativeLaunchTooLarge;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if ((e = hipStreamIsCapturing(s, &cap)) != hipSuccess) return e;
-    if (cap != hipStreamCaptureStatusNone) return hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s);
+    if (cap != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
     constexpr int kMaxDev = 64;
     struct Serial {
         std::mutex mu;
@@ -108,7 +112,13 @@ hipError_t launch_coresident_raw(const void *fn, int grid, int block, size_t lds
     // an event never recorded counts as complete, so the first wait is free
     if ((e = hipStreamWaitEvent(s, sd.last, 0)) != hipSuccess) return e;
     if ((e = hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, s)) != hipSuccess) return e;
-    return hipEventRecord(sd.last, s);
+    if (hipEventRecord(sd.last, s) != hipSuccess) {
+        // the grid is running but the next co-resident grid could not be
+        // ordered after it: drain the stream here instead (the event, never
+        // re-recorded, still reads complete), so the launch itself succeeds
+        (void)hipStreamSynchronize(s);
+    }
+    return hipSuccess;
 }
 }  // namespace fpm
 
@@ -192,6 +202,8 @@ struct fpm_ctx {
     bool uploaded = false, initialized = false, objcrop_valid = false;
     std::vector<hipEvent_t> evpool;
     unsigned long long *dbg = nullptr;  // FPM_STAMPS=1: fused-kernel phase cycles
+    unsigned long long *clk = nullptr;  // fused kernels' launch clock probe [3] (ClockProbe)
+    fpm_clock clock{};                  // of the most recent fpm_run
     fpm_timing timing{};
     // general path: one iteration's 4*n_order launches captured once and
     // replayed as a single graph launch (FPM_NO_GRAPH=1 launches them directly)
@@ -474,6 +486,12 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     }
     st.meas = c->meas;
     st.disk = c->disk_dev;
+    if (c->path == FPM_PATH_FUSED) {
+        if ((rc = dalloc(c, &c->clk, 3))) return fail(rc);
+        if (hipMemset(c->clk, 0, 3 * sizeof(unsigned long long)) != hipSuccess)
+            return fail(set_err(FPM_ERR_DEVICE, "memset failed"));
+        st.clk = c->clk;
+    }
     if (getenv("FPM_STAMPS") && c->path == FPM_PATH_FUSED) {
         if ((rc = dalloc(c, &c->dbg, 2 * kStamps))) return fail(rc);
         if (hipMemset(c->dbg, 0, 2 * kStamps * sizeof(unsigned long long)) != hipSuccess)
@@ -718,6 +736,15 @@ int fpm_run(fpm_ctx *c, int iters) {
     if (!c->initialized) return set_err(FPM_ERR_STATE, "fpm_run before fpm_init");
     if (iters < 0) return set_err(FPM_ERR_INVAL, "iters=%d", iters);
     HIP_TRY(hipSetDevice(c->device));
+    {   // blocking (event waits, the abort-word read-back): never inside a capture
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(c->stream, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            return set_err(FPM_ERR_INVAL, "fpm_run on a capturing stream: fpm_run is blocking and its %s cannot be "
+                           "replayed from a graph (fpm_hip.h)",
+                           c->split_ks > 1 ? "co-resident grids" : "launches");
+    }
+    if (c->clk) HIP_TRY(hipMemsetAsync(c->clk, 0, 3 * sizeof(unsigned long long), c->stream));
     const bool last_only = (c->prob.flags & FPM_FLAG_OBJCROP_LAST_ONLY) != 0;
     // one event pair per iteration around the LED-update launches, one pair
     // around the objCrop IDFT; read back once at the end (fpm_run is blocking)
@@ -814,6 +841,27 @@ int fpm_run(fpm_ctx *c, int iters) {
         }
     }
     c->timing.led_launch_ms = c->timing.led_launches ? led_ms / c->timing.led_launches : 0.0;
+    c->clock = fpm_clock{};
+    if (c->clk) {
+        unsigned long long h[3] = {0, 0, 0};
+        HIP_TRY(hipMemcpy(h, c->clk, sizeof h, hipMemcpyDeviceToHost));
+        int khz = 0;  // s_memrealtime rate
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        if (h[2] > 0 && h[1] > 0) {
+            const double sec = (double)h[1] / (khz * 1e3);
+            c->clock.clock_mhz = (double)h[0] / sec / 1e6;
+            c->clock.cycles_per_launch = (double)h[0] / (double)h[2];
+            c->clock.ms_per_launch = sec * 1e3 / (double)h[2];
+            c->clock.launches = (int32_t)h[2];
+        }
+    }
+    return FPM_OK;
+}
+
+int fpm_get_clock(const fpm_ctx *c, fpm_clock *clock) {
+    if (!c || !clock) return set_err(FPM_ERR_INVAL, "null argument");
+    *clock = c->clock;
     return FPM_OK;
 }
 

@@ -343,13 +343,16 @@ __device__ __forceinline__ float row16_sum(float v) {
     v += dpp_f<0x121>(v);  // row_ror:1
     return v;
 }
-// Every caller reduces values >= +0 (magnitudes, |z|^2, tile maxima), whose
-// IEEE bits order as unsigned integers: the steps are v_max_u32 (fmaxf costs a
-// canonicalising v_max per operand in IEEE mode: three VALU per step instead
-// of one) and the four row maxima fold on the scalar unit.  A NaN would win
-// here where fmaxf drops it -- it never reaches a maximum of a finite run.
-__device__ __forceinline__ float wave_max(float x) {
-    unsigned v = __float_as_uint(x);
+// For values >= +0 only (magnitudes, |z|^2, tile maxima -- every caller),
+// whose IEEE bits order as unsigned integers: the steps are v_max_u32 (fmaxf
+// costs a canonicalising v_max per operand in IEEE mode: three VALU per step
+// instead of one) and the four row maxima fold on the scalar unit.  The sign
+// bit is cleared on entry, so a misuse with a negative input (or -0) reduces
+// |x| -- a bounded result, never a negative value winning as a huge unsigned
+// one.  A NaN would win here where fmaxf drops it -- it never reaches a
+// maximum of a finite run.
+__device__ __forceinline__ float wave_max_nonneg(float x) {
+    unsigned v = __float_as_uint(x) & 0x7fffffffu;
     auto dpp_u = [](unsigned u, auto ctrl) {
         // old = 0, the identity of unsigned max: the DPP combiner folds the
         // move into the v_max_u32 that uses it
@@ -364,12 +367,12 @@ __device__ __forceinline__ float wave_max(float x) {
     return __uint_as_float(max(max(r0, r1), max(r2, r3)));
 }
 
-// Max over the block; `red` is LDS scratch of >= nwaves floats. Result valid
-// in every thread. Contains two barriers.
-__device__ __forceinline__ float block_max(float v, float *red) {
+// Max over the block of values >= +0 (wave_max_nonneg); `red` is LDS scratch
+// of >= nwaves floats. Result valid in every thread. Contains two barriers.
+__device__ __forceinline__ float block_max_nonneg(float v, float *red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nw = (blockDim.x + 63) >> 6;
-    v = wave_max(v);
+    v = wave_max_nonneg(v);
     if (lane == 0) red[w] = v;
     __syncthreads();
     float r = red[0];

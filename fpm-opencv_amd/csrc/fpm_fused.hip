@@ -77,6 +77,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     using namespace fz;
     using C = FzCfg<NT>;
     constexpr int NG = C::NG, RPG = C::RPG, NW = C::NW;
+    ClockProbe probe;
+    probe.start();
     static_assert(KS == 1 || KS == 2 || KS == 4, "one workgroup per patch, or split mode with 2 / 4");
     static_assert(6 * RPG * 16 <= C::XT, "pupil numerators are parked in the group's exchange tile");
     constexpr int NPARTS = n_parts(KS), TH = part_cols(KS), TLD = TH + 1;
@@ -645,8 +647,8 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             if (d) dm = fmaxf(dm, tmx[k]);
             else cm = fmaxf(cm, tmx[k]);
         }
-        cm = wave_max(cm);
-        dm = wave_max(dm);
+        cm = wave_max_nonneg(cm);
+        dm = wave_max_nonneg(dm);
         if (lane == 0) {
             red[w] = cm;
             red[16 + w] = dm;
@@ -673,7 +675,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 float mm = 0.f;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) mm = fmaxf(mm, cmag(e[jj]));
-                mm = wave_max(mm);
+                mm = wave_max_nonneg(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
                     atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
@@ -683,7 +685,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
             float m2 = 0.f;
             for (int k = tid; k < a.nbt; k += NT)
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
-            m2 = wave_max(m2);
+            m2 = wave_max_nonneg(m2);
             __syncthreads();  // red[] reads above are done
             if (lane == 0) red[w] = m2;
             __syncthreads();
@@ -714,7 +716,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         // max|P| is first needed by the next LED's object update, several
         // barriers later: it is reduced there (pm_of_red), not behind a
         // barrier of its own here.
-        pmx = wave_max(pmx);
+        pmx = wave_max_nonneg(pmx);
         if (lane == 0) red[32 + w] = pmx;
         pupil_done = true;
         FPM_STAMP(6)
@@ -722,6 +724,7 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
     }
 #undef FPM_STAMP
     __syncthreads();  // the last LED's red[32..]
+    probe.stop(a.st.clk);
     if (pupil_done) pm = pm_of_red();
     // stamps of the first and the last wave (the barrier waits show who is slow)
     // (split mode: the first wave of the first and of the last part's workgroup)
@@ -834,7 +837,7 @@ hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, cons
     const size_t lds0 = fused_lds_bytes(ks, a.nbt, g.n_tail_rows);
     if (lds0 > 160 * 1024) return hipErrorInvalidValue;
     size_t lds;  // + the LED table when it fits
-    a.ledtab_off = ledtab_offset(lds0, n_order, 160 * 1024, lds);
+    a.ledtab_off = ledtab_offset(lds0, n_order, st.L, 160 * 1024, lds);
     const void *fn = ks == 4   ? (const void *)k_fused_iteration<512, 4>
                      : ks == 2 ? (const void *)k_fused_iteration<512, 2>
                                : (const void *)k_fused_iteration<512, 1>;

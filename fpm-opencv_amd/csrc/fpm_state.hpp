@@ -80,6 +80,9 @@ struct DevState {
     // layout of meas: 0 = C-ABI [led][patch][y][x]; g > 0 = the fused kernels'
     // column layout [led][patch][x][t][m] = I[t + g m][x] (meas_layout)
     int meas_g;
+    // launch clock probe of the fused kernels (fused_sync.hpp ClockProbe):
+    // [3] = block 0's shader cycles, 100 MHz ticks, launches; null = off
+    unsigned long long *clk;
 };
 
 // patches [b0, b0 + n) of a context as a DevState of n patches (the general

@@ -65,6 +65,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     constexpr int CB = TH / 4 < 16 ? TH / 4 : 16;      // pass-B block: columns (r8 % CB) + CB gg + 4 CB (r8 / CB)
     constexpr int NBLK = TH / 4;
     static_assert(KS == 2 || KS == 4 || KS == 8, "two, four or eight parts");
+    ClockProbe probe;
+    probe.start();
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
     float2 *scr_all = sm;                           // NG * XTILE exchange tiles
@@ -341,8 +343,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                     if ((dirty[k >> 5] >> (k & 31)) & 1u) d = fmaxf(d, v);
                     else c = fmaxf(c, v);
                 }
-                c = wave_max(c);
-                d = wave_max(d);
+                c = wave_max_nonneg(c);
+                d = wave_max_nonneg(d);
                 if (lane == 0) {
                     atomicMax(&omx[0], __float_as_uint(c));
                     atomicMax(&omx[1], __float_as_uint(d));
@@ -599,8 +601,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // the merge wave folds the window tiles into the outside maxima
         if (w == WMERGE) {
             float c = wdirty ? 0.f : wcm, d = wdirty ? wcm : 0.f;
-            c = wave_max(c);
-            d = wave_max(d);
+            c = wave_max_nonneg(c);
+            d = wave_max_nonneg(d);
             if (lane == 0) {
                 red[0] = fmaxf(c, __uint_as_float(omx[0]));
                 red[16] = fmaxf(d, __uint_as_float(omx[1]));
@@ -626,7 +628,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
                 float mm = 0.f;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) mm = fmaxf(mm, cmag(e[jj]));
-                mm = wave_max(mm);
+                mm = wave_max_nonneg(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
                     atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
@@ -636,7 +638,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             float m2 = 0.f;
             for (int k = tid; k < a.nbt; k += NT)
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
-            m2 = wave_max(m2);
+            m2 = wave_max_nonneg(m2);
             __syncthreads();
             if (lane == 0) red[w] = m2;
             __syncthreads();
@@ -660,12 +662,13 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             Pt = make_float2(Pt.x + NPt.x * rom, Pt.y + NPt.y * rom);
             pmx = fmaxf(pmx, cabs2(Pt));
         }
-        pmx = wave_max(pmx);
+        pmx = wave_max_nonneg(pmx);
         if (lane == 0) red[32 + w] = pmx;
         FPM_STAMP(10)
     }
 #undef FPM_STAMP
     __syncthreads();  // red[32..]
+    probe.stop(a.st.clk);
     if (a.dbg && tid == 0 && (hown == 0 || hown == KS - 1))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(hown ? kStamps : 0) + i], acc[i]);
     // ---- write back: each part its own pupil rows and tail pixels; part 0
@@ -775,7 +778,7 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     const size_t lds0 = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
     if (lds0 > 160 * 1024) return hipErrorInvalidValue;
     size_t lds;  // + the LED table when it fits
-    a.ledtab_off = ledtab_offset(lds0, n_order, 160 * 1024, lds);
+    a.ledtab_off = ledtab_offset(lds0, n_order, st.L, 160 * 1024, lds);
     const void *fn = ks == 8   ? (const void *)k_fused_dist<8>
                      : ks == 4 ? (const void *)k_fused_dist<4>
                                : (const void *)k_fused_dist<2>;

@@ -39,6 +39,7 @@
 #include "dft200.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
+#include "fused_sync.hpp"
 #include "ledtab.hpp"
 #include "tilemax.hpp"
 #include "update.hpp"
@@ -101,6 +102,8 @@ __device__ __forceinline__ int mr_kx(int l, int s) { return l + 10 * fm::SK[s] -
 
 __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
     using namespace fm;
+    ClockProbe probe;
+    probe.start();
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const DevState &st = a.st;
     const int R = st.r, NB = st.nb, L = st.L;
@@ -376,7 +379,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
                     if (ok[jj]) mm = fmaxf(mm, cmag(e[jj]));
-                mm = wave_max(mm);
+                mm = wave_max_nonneg(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
                     atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
@@ -386,7 +389,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
             float m2 = 0.f;
             for (int k = tid; k < a.nbt; k += NT)
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
-            m2 = wave_max(m2);
+            m2 = wave_max_nonneg(m2);
             __syncthreads();
             if (lane == 0) red[w] = m2;
             __syncthreads();
@@ -408,7 +411,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         }
         // max|P| partials per wave, folded after the next LED's A barrier (the
         // next update is the first use): this phase needs no barrier
-        pmx = wave_max(pmx);
+        pmx = wave_max_nonneg(pmx);
         if (lane == 0) red[32 + w] = pmx;
         FPM_STAMP(6)
     }
@@ -423,6 +426,7 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         __syncthreads();  // the last LED's red[32..]
         pm = fold_pm();
     }
+    probe.stop(st.clk);
     // stamps of the first and the last wave (the barrier waits show who is slow)
     if (a.dbg && (tid == 0 || tid == NT - 64))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
@@ -481,7 +485,7 @@ hipError_t launch_fused_mr_iteration(const DevState &st, const uint16_t *meas, c
     for (int i = 0; i < fm::GPW; ++i)
         a.xg[i] = a.xw == fm::XW_SHIFT ? fm::XG_SHIFT[i] : i * (a.xw == fm::XW_STRIDE ? 106 : fm::XT);
     size_t lds;  // the kernel's own LDS + the LED table when it fits
-    a.ledtab_off = ledtab_offset(mr_lds_bytes(st.nb, a.nbt, a.xw, a.tld), n_order, 160 * 1024, lds);
+    a.ledtab_off = ledtab_offset(mr_lds_bytes(st.nb, a.nbt, a.xw, a.tld), n_order, st.L, 160 * 1024, lds);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_mr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_mr, dim3(st.B), dim3(fm::NT), lds, s, a);

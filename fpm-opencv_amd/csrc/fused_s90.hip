@@ -31,6 +31,7 @@
 #include "dft90.hpp"
 #include "fft_lds.hpp"
 #include "fpm_state.hpp"
+#include "fused_sync.hpp"
 #include "ledtab.hpp"
 #include "tilemax.hpp"
 #include "update.hpp"
@@ -85,6 +86,8 @@ __device__ __forceinline__ int f90_fold(int n) { return n < f90::NP / 2 ? n : n 
 
 __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
     using namespace f90;
+    ClockProbe probe;
+    probe.start();
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const DevState &st = a.st;
     const int R = st.r, NB = st.nb, L = st.L;
@@ -344,7 +347,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
                     if (ok[jj]) mm = fmaxf(mm, cmag(e[jj]));
-                mm = wave_max(mm);
+                mm = wave_max_nonneg(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
                     atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
@@ -354,7 +357,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
             float m2 = 0.f;
             for (int k = tid; k < a.nbt; k += NT)
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
-            m2 = wave_max(m2);
+            m2 = wave_max_nonneg(m2);
             __syncthreads();
             if (lane == 0) red[w] = m2;
             __syncthreads();
@@ -376,7 +379,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         }
         // max|P| partials per wave; folded after the next LED's A barrier (the
         // next update is its first use), so this phase needs no barrier
-        pmx = wave_max(pmx);
+        pmx = wave_max_nonneg(pmx);
         if (lane == 0) red[32 + w] = pmx;
         FPM_STAMP(6)
     }
@@ -391,6 +394,7 @@ __global__ void __launch_bounds__(f90::NT, 1) k_fused_s90(FusedS90Args a) {
         pm = fold_pm();
     }
 #undef FPM_STAMP
+    probe.stop(st.clk);
     if (a.dbg && (tid == 0 || tid == NT - 64))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(tid ? kStamps : 0) + i], acc[i]);
 
@@ -444,7 +448,7 @@ hipError_t launch_fused_s90_iteration(const DevState &st, const uint16_t *meas, 
     a.tld = fast ? f90::TLD_FAST : f90::TLD;
     a.dbg = dbg;
     size_t lds;  // the kernel's own LDS + the LED table when it fits
-    a.ledtab_off = ledtab_offset(s90_lds_bytes(st.nb, a.nbt, a.xw, a.tld), n_order, 160 * 1024, lds);
+    a.ledtab_off = ledtab_offset(s90_lds_bytes(st.nb, a.nbt, a.xw, a.tld), n_order, st.L, 160 * 1024, lds);
     hipError_t e = hipFuncSetAttribute((const void *)k_fused_s90, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fused_s90, dim3(st.B), dim3(f90::NT), lds, s, a);

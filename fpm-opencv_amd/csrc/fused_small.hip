@@ -294,8 +294,8 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             if (d) dm = fmaxf(dm, tmx[k]);
             else cm = fmaxf(cm, tmx[k]);
         }
-        cm = wave_max(cm);
-        dm = wave_max(dm);
+        cm = wave_max_nonneg(cm);
+        dm = wave_max_nonneg(dm);
         if (lane == 0) {
             red[w] = cm;
             red[16 + w] = dm;
@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
                     if (ok[jj]) mm = fmaxf(mm, cmag(e[jj]));
-                mm = wave_max(mm);
+                mm = wave_max_nonneg(mm);
                 if (lane == 0) {
                     tmx[k] = mm;
                     atomicAnd(&dirty[k >> 5], ~(1u << (k & 31)));
@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             float m2 = 0.f;
             for (int k = tid; k < a.nbt; k += NT)
                 if (!((dirty[k >> 5] >> (k & 31)) & 1u)) m2 = fmaxf(m2, tmx[k]);
-            m2 = wave_max(m2);
+            m2 = wave_max_nonneg(m2);
             __syncthreads();
             if (lane == 0) red[w] = m2;
             __syncthreads();
@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(fs::NT, 1) k_fused_small(SmallArgs a) {
             P[i] = make_float2(P[i].x + NUM[i].x * rom, P[i].y + NUM[i].y * rom);
             pmx = fmaxf(pmx, cabs2(P[i]));
         }
-        pmx = wave_max(pmx);
+        pmx = wave_max_nonneg(pmx);
         if (lane == 0) red[32 + w] = pmx;
         __syncthreads();
         float pm2 = red[32];

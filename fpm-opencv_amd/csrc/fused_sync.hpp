@@ -91,6 +91,29 @@ __device__ __forceinline__ bool handoff_wait(int *flags, int me, int value, int 
     return *okslot != 0;
 }
 
+// Launch clock probe (the bench line's clock_mhz / kernel_cycles_per_launch,
+// MI355X_MICROARCH.md DVFS item 6): block 0's shader cycles (s_memtime) and
+// 100 MHz real-time ticks (s_memrealtime) from kernel entry to its last
+// phase, summed into clk[0] / clk[1] with clk[2] counting launches.  Read in
+// every wave as wave-uniform scalars (no VGPRs held across the kernel);
+// thread 0 of block 0 accumulates with vector atomics into the context's own
+// probe buffer, which nothing else reads.  Two SMEM reads per wave per launch.
+struct ClockProbe {
+    unsigned long long c0, r0;
+    __device__ __forceinline__ void start() {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ void stop(unsigned long long *clk) const {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (clk && blockIdx.x == 0 && threadIdx.x == 0) {
+            atomicAdd(clk, c1 - c0);
+            atomicAdd(clk + 1, r1 - r0);
+            atomicAdd(clk + 2, 1ull);
+        }
+    }
+};
+
 // measurement stream: read once per LED, so load it non-temporally and keep
 // L2 for the spectrum window the next LED re-reads
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));

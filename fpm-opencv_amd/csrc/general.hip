@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(256) k_rowfft_update(DevState st, StepArgs sa,
     __shared__ float red[4];
     float pm = 0.f;
     for (int i = threadIdx.x; i < st.npart; i += blockDim.x) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
-    pm = block_max(pm, red);
+    pm = block_max_nonneg(pm, red);
     const int yrow = sa.yc + ky;
     for (int j = threadIdx.x; j < nb; j += blockDim.x) {
         if (!st.disk[row * nb + j]) continue;
@@ -200,12 +200,12 @@ __global__ void __launch_bounds__(kRowThreads) k_tile_rows(DevState st, StepArgs
         for (int i = 0; i < MT; ++i) {
             const int tx = base + i * NW;
             if (tx > tx1) break;  // wave-uniform
-            const float t = wave_max(m[i]);
+            const float t = wave_max_nonneg(m[i]);
             if (lane == 0) tmax[tx] = t;
             mx = fmaxf(mx, t);
         }
     }
-    mx = block_max(mx, red);
+    mx = block_max_nonneg(mx, red);
     if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = mx;
 }
 
@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(kCommitThreads) k_pupil_commit(DevState st) {
     }
     float m = 0.f;
     for (int i = threadIdx.x; i < st.nty; i += kCommitThreads) m = fmaxf(m, rmax[i]);
-    const float omax = block_max(m, red);
+    const float omax = block_max_nonneg(m, red);
     float pm = 0.f;
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(kCommitThreads) k_pupil_commit(DevState st) {
         pup[i0 + threadIdx.x + k * kCommitThreads] = p;
         pm = fmaxf(pm, cmag(p));
     }
-    pm = block_max(pm, red);
+    pm = block_max_nonneg(pm, red);
     if (threadIdx.x == 0) st.pmax[b * st.npart + part] = pm;
 }
 
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(E <= 16
     // max|P| of the previous commit from its npart partial maxima
     float pm = 0.f;
     for (int i = threadIdx.x; i < st.npart; i += NT) pm = fmaxf(pm, st.pmax[b * st.npart + i]);
-    pm = block_max(pm, red);  // its barriers also publish the tile
+    pm = block_max_nonneg(pm, red);  // its barriers also publish the tile
     tile_transform_ex<false, NT, E>(tile, pl, lc, lss, 1, stw);                             // :394
     float2 *pup = st.pupil + (size_t)b * nb * nb;
     float2 *dP = st.dP + (size_t)b * nb * nb;
@@ -813,7 +813,7 @@ __global__ void __launch_bounds__(256) k_tile_max_all(DevState st) {
     const int y = ty * kTile + (threadIdx.x >> 4), x = tx * kTile + (threadIdx.x & 15);
     float m = 0.f;
     if (y < L && x < L) m = cmag(spec_ld(st, b, (size_t)y * L + x));
-    m = block_max(m, red);
+    m = block_max_nonneg(m, red);
     if (threadIdx.x == 0) st.tmax[(size_t)b * st.nty * st.ntx + t] = m;
 }
 
@@ -824,7 +824,7 @@ __global__ void __launch_bounds__(256) k_row_max_all(DevState st) {
     const float *tm = st.tmax + ((size_t)b * st.nty + ty) * st.ntx;
     float m = 0.f;
     for (int i = threadIdx.x; i < st.ntx; i += 256) m = fmaxf(m, tm[i]);
-    m = block_max(m, red);
+    m = block_max_nonneg(m, red);
     if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = m;
 }
 

@@ -32,7 +32,9 @@ struct LedTab {
     __device__ __forceinline__ LedPos at(int it) const {
         if (lds) {
             const int2 e = lds[it];
-            return LedPos{e.x, e.y >> 16, e.y & 0xffff};
+            // centres are in [0, L): unsigned 16-bit fields (ledtab_offset
+            // refuses the table for L > 65536)
+            return LedPos{e.x, (int)((unsigned)e.y >> 16), (int)((unsigned)e.y & 0xffffu)};
         }
         const int led = order[it];
         return LedPos{led, y0[led] + half, x0[led] + half};
@@ -41,10 +43,12 @@ struct LedTab {
 
 // Host: byte offset of the table after `lds` bytes of a kernel's own LDS
 // (8-byte aligned), or -1 when it does not fit in `cap` bytes; `total`
-// becomes the launch's dynamic LDS size.  Centres need 16 bits (L <= 65535).
-inline int ledtab_offset(size_t lds, int n_order, size_t cap, size_t &total) {
+// becomes the launch's dynamic LDS size.  A centre (yc, xc) lies in [0, L)
+// (fpm_create keeps every crop window inside the spectrum) and is packed as
+// two unsigned 16-bit fields, so the table is used only for L <= 65536.
+inline int ledtab_offset(size_t lds, int n_order, int L, size_t cap, size_t &total) {
     const size_t off = (lds + 7) & ~(size_t)7;
-    if (n_order > 0 && off + (size_t)n_order * 8 <= cap) {
+    if (n_order > 0 && L <= 65536 && off + (size_t)n_order * 8 <= cap) {
         total = off + (size_t)n_order * 8;
         return (int)off;
     }

@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
         for (int k = 0; k < 2; ++k)
             if ((int)threadIdx.x + NT * k < st.nty) m = fmaxf(m, rm[k]);
         for (int i = threadIdx.x + 2 * NT; i < st.nty; i += NT) m = fmaxf(m, st.rmax[(size_t)b * st.nty + i]);  // L > 8192 only
-        omax = block_max(m, red);
+        omax = block_max_nonneg(m, red);
     }
     if (row >= nb) return;  // wave-uniform; no block barrier follows
     auto body = [&](int j, float2 p, float2 d, float2 o) {
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
             for (int i = 0; i < 8; ++i) body(8 * hh + i, q.pv[i], q.dv[i], q.ov[i]);
         }
     }
-    pmx = wave_max(pmx);
+    pmx = wave_max_nonneg(pmx);
     if (lane == 0) st.pmax[(size_t)b * st.npart + row] = pmx;
     w1k_DN<true>(x, wt, twL, c, t, xrd);                                 // :365 (rows)
     if (st.T16) {  // fp16 scratch: one power-of-two scale per box row
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
         for (int j = 0; j < 16; ++j) m = fmaxf(m, fmaxf(fabsf(x[j].x), fabsf(x[j].y)));
         float inv;
-        const float sc = h16_scale(wave_max(m), &inv);
+        const float sc = h16_scale(wave_max_nonneg(m), &inv);
         __half2 *T = st.T16 + ((size_t)b * nb + row) * N + t + 64 * c;
 #pragma unroll
         for (int p = 0; p < 4; ++p)
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
         for (int j = 0; j < 16; ++j) m = fmaxf(m, fmaxf(fabsf(x[j].x), fabsf(x[j].y)));
         float inv;
-        sc = h16_scale(wave_max(m), &inv);
+        sc = h16_scale(wave_max_nonneg(m), &inv);
         if ((threadIdx.x & 63) == 0) st.tsc[(size_t)b * N + x0 + w] = inv;
     }
     __syncthreads();  // every wave is done with its tile before the strip is rewritten
@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
         if ((int)threadIdx.x + NT * k < st.npart) pm = fmaxf(pm, pv4[k]);
 #pragma unroll
     for (int i = 0; i < N / NT; ++i) sm[threadIdx.x + NT * i] = twv[i];
-    pm = block_max(pm, red);
+    pm = block_max_nonneg(pm, red);
     if (row >= nb) return;
     const int ky = row - r, w2 = r * r - ky * ky;
     if (st.T16) {  // column j's element times its column scale

@@ -50,8 +50,8 @@ __device__ __forceinline__ void outside_max(const float *tmx, const unsigned *di
         if (tile_dirty(dirty, k)) dd = fmaxf(dd, v);
         else cc = fmaxf(cc, v);
     }
-    c = wave_max(cc);
-    d = wave_max(dd);
+    c = wave_max_nonneg(cc);
+    d = wave_max_nonneg(dd);
 }
 
 // After the update (tiles final): the band's clean maximum cm and dirty
@@ -69,8 +69,8 @@ __device__ __forceinline__ void window_max(const float *tmx, const unsigned *dir
         if (tile_dirty(dirty, k)) dd = fmaxf(dd, v);
         else cc = fmaxf(cc, v);
     }
-    cm = wave_max(cc);
-    dm = wave_max(dd);
+    cm = wave_max_nonneg(cc);
+    dm = wave_max_nonneg(dd);
 }
 
 }  // namespace fpm

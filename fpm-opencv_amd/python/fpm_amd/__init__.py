@@ -49,10 +49,11 @@ HIP_SYMBOLS = (
     "fpm_download_objcrop_device", "fpm_set_stream", "fpm_get_info",
     "fpm_get_timing", "fpm_runFPM", "fpm_last_error", "fpm_version",
     "fpm_upload_frames", "fpm_download_stack", "fpm_get_info_sized", "fpm_abi_version",
+    "fpm_get_clock",
 )
 # test-only entry points (include/fpm_hip_debug.h)
 HIP_DEBUG_SYMBOLS = ("fpm_debug_slot_update", "fpm_debug_update_coef", "fpm_debug_set_stall")
-ABI_VERSION = 4  # include/fpm_hip.h FPM_ABI_VERSION this mirror follows
+ABI_VERSION = 5  # include/fpm_hip.h FPM_ABI_VERSION this mirror follows
 
 
 class FpmError(RuntimeError):
@@ -94,6 +95,11 @@ class fpm_timing(C.Structure):
                 ("objcrop_ms", C.c_double)]
 
 
+class fpm_clock(C.Structure):
+    _fields_ = [("clock_mhz", C.c_double), ("cycles_per_launch", C.c_double),
+                ("ms_per_launch", C.c_double), ("launches", C.c_int32)]
+
+
 _lib = None
 
 
@@ -125,6 +131,7 @@ def load_library(path: str = HIP_LIB):
         "fpm_abi_version": (C.c_int, []),
         "fpm_debug_set_stall": (C.c_int, [vp, C.c_int]),
         "fpm_get_timing": (C.c_int, [vp, C.POINTER(fpm_timing)]),
+        "fpm_get_clock": (C.c_int, [vp, C.POINTER(fpm_clock)]),
         "fpm_runFPM": (C.c_int, [C.POINTER(fpm_problem), C.c_int, u16p, C.c_int,
                                  f32p, f32p, f32p, f32p]),
         "fpm_upload_frames": (C.c_int, [vp, C.POINTER(fpm_frames), vp, C.c_int, C.POINTER(C.c_int16)]),
@@ -308,6 +315,13 @@ class Solver:
         t = fpm_timing()
         _check(_lib.fpm_get_timing(self._h, C.byref(t)))
         return t
+
+    def clock(self) -> fpm_clock:
+        """Shader clock and cycles of the last run's LED-update launches
+        (fused path; launches == 0 on the general path)."""
+        k = fpm_clock()
+        _check(_lib.fpm_get_clock(self._h, C.byref(k)))
+        return k
 
 
 def run_fpm(prob: Problem, stack: np.ndarray, iters: int, device: int = 0):

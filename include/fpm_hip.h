@@ -30,9 +30,12 @@ extern "C" {
 #endif
 
 /* ABI revision of this header.  Round 4 (4): fpm_info gained threads_per_wg,
- * readable only through fpm_get_info_sized (fpm_get_info keeps writing the
- * ABI-3 struct size).  fpm_abi_version() reports the library's revision. */
-#define FPM_ABI_VERSION   4
+ * readable only through fpm_get_info_sized.  Round 6 (5): fpm_get_info writes
+ * only the ABI-3 struct size (path .. fused_kernel) -- under ABI 4 it wrote
+ * the whole struct, so a caller reading threads_per_wg from it must move to
+ * fpm_get_info_sized; fpm_get_clock added; fpm_run refuses a capturing
+ * stream.  fpm_abi_version() reports the library's revision. */
+#define FPM_ABI_VERSION   5
 
 #define FPM_OK            0
 #define FPM_ERR_INVAL   (-22)   /* bad argument / unsupported geometry      */
@@ -182,7 +185,12 @@ int  fpm_init(fpm_ctx *ctx);
 /* fpmMain.cpp:345-482: `iters` sequential passes over order[], each followed
  * by the objCrop IDFT (fpmMain.cpp:481) unless FPM_FLAG_OBJCROP_LAST_ONLY.
  * Enqueued on the context stream; returns when the work has completed
- * (per-kernel HIP-event timings are then available from fpm_get_timing). */
+ * (per-kernel HIP-event timings are then available from fpm_get_timing).
+ * Blocking, so it cannot be recorded into a graph: on a stream that is being
+ * captured it returns FPM_ERR_INVAL before enqueuing anything (the capture
+ * stays valid).  The split / distributed modes also need every workgroup of
+ * a grid resident at once, which a replayed graph could not guarantee
+ * beside other co-resident grids. */
 int  fpm_run(fpm_ctx *ctx, int iters);
 
 /* Wait for all work on the context stream. */
@@ -212,6 +220,21 @@ int  fpm_set_stream(fpm_ctx *ctx, void *hip_stream);
 int  fpm_get_info(const fpm_ctx *ctx, fpm_info *info);
 int  fpm_get_info_sized(const fpm_ctx *ctx, fpm_info *info, size_t info_size);
 int  fpm_get_timing(const fpm_ctx *ctx, fpm_timing *timing);
+
+/* Clock of the LED-update launches of the most recent fpm_run (fused path;
+ * ABI 5): block 0 of every launch reads the shader-cycle counter (s_memtime)
+ * and the constant-rate real-time counter (s_memrealtime) at entry and after
+ * its last LED, so clock_mhz = cycles / real time is the shader clock the
+ * kernel actually ran at and cycles_per_launch its length in cycles, which a
+ * slower clock does not change (MI355X_MICROARCH.md, DVFS).  launches = 0 on
+ * the general path, which has no probe. */
+typedef struct fpm_clock {
+    double clock_mhz;          /* mean shader clock over the probed launches   */
+    double cycles_per_launch;  /* block 0's shader cycles per launch           */
+    double ms_per_launch;      /* block 0's real time per launch               */
+    int32_t launches;          /* launches probed                              */
+} fpm_clock;
+int  fpm_get_clock(const fpm_ctx *ctx, fpm_clock *clock);
 
 /* One-shot equivalent of runFPM for n_patch patches: create, upload, init,
  * run, download, destroy.  Blocking. */

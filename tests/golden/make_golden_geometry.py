@@ -31,6 +31,9 @@ CASES = [
     # SURVEY.md 8(c) fallback: dataset_mono.json optics with the 508-LED dome
     # table of include/domeHoleCoordinates.h inserted as holeCoordinates
     ("mono_dome", "dataset_mono.json+dome", 508, None, None),
+    # the same at cropSizeX 256 (Np 256, L 1024, naRadius 84,
+    # 193 LEDs; BASELINE.md 3 "dataset_mono geometry (Np = 90 / 256)")
+    ("mono_dome_np256", "dataset_mono.json+dome", 508, 0.45, 256),
 ]
 DOME_H = "include/domeHoleCoordinates.h"
 

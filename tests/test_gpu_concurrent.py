@@ -77,6 +77,55 @@ def test_two_coresident_contexts_on_two_streams():
             s.close()
 
 
+def test_run_on_a_capturing_stream_is_refused():
+    """fpm_run is blocking and, in distributed / split mode, launches grids
+    whose workgroups must all be resident at once; a replayed graph could not
+    keep them ordered against other co-resident grids, so a capturing caller
+    stream is refused with FPM_ERR_INVAL before anything is enqueued
+    (fpm_hip.h).  The capture stays valid and the context
+    runs normally afterwards."""
+    import torch
+    B = 64
+    prob, st = _problem(B, 73)
+    with fpm_amd.Solver(prob) as s:
+        info = s.info()
+        assert info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256_DIST and info.wg_per_patch * B == 256
+        s.upload(st)
+        s.init()
+        s.run(1)
+        want = s.download(objF=False, support=False)
+        s.init()
+        cs = torch.cuda.Stream()
+        s.set_stream(cs.cuda_stream)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with pytest.raises(fpm_amd.FpmError) as ei:
+            with torch.cuda.graph(g, stream=cs, capture_error_mode="relaxed"):
+                s.run(1)
+        assert ei.value.code == fpm_amd.FPM_ERR_INVAL and "capturing" in str(ei.value)
+        s.set_stream(None)
+        s.run(1)  # the refused call left the context usable
+        got = s.download(objF=False, support=False)
+        for k in ("objCrop", "pupil"):
+            assert np.array_equal(got[k], want[k]), k
+
+
+def test_clock_probe_reports_the_launch():
+    """fpm_get_clock (ABI 5): block 0's shader cycles and real time over each
+    LED-update launch; the clock they give is a plausible MI355X shader clock
+    and the probed time agrees with the HIP-event launch time."""
+    prob, st = _problem(8, 74)
+    with fpm_amd.Solver(prob) as s:
+        s.upload(st)
+        s.init()
+        s.run(3)
+        k, t = s.clock(), s.timing()
+        assert k.launches == 3
+        assert 500.0 < k.clock_mhz < 2600.0, k.clock_mhz
+        assert k.cycles_per_launch > 0
+        assert 0.5 * t.led_launch_ms < k.ms_per_launch <= 1.05 * t.led_launch_ms, (k.ms_per_launch, t.led_launch_ms)
+
+
 def test_get_info_writes_only_the_abi3_struct():
     """fpm_get_info is frozen at the ABI-3 layout (path .. fused_kernel): a
     caller built against that header has a struct of that size, so nothing

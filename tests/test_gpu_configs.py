@@ -97,6 +97,40 @@ def _tiled_stack(Np, L, r, x0, y0, B, n_distinct, seed):
     return base[:, idx], idx
 
 
+def test_config2_geometry_at_np256_r84_64_patches():
+    """BASELINE.md 3's "dataset_mono geometry (Np = 90 / 256)" at Np 256: the
+    dome fallback at cropSizeX 256 (tests/golden/geometry_mono_dome_np256.json
+    from the reference's own jsoncpp probe) gives L 1024 and naRadius 84
+    (fpmMain.cpp:305-306), beyond the fused Np 256 kernels' r <= 34, so the
+    general path runs it (fpm_info); 64 patches, 2 iterations, sampled patches
+    vs the C++ fp64 oracle."""
+    import oracle_lib
+    p, x0, y0 = _probe_geometry("geometry_mono_dome_np256.json")
+    Np, L, r = p["np"], p["nlarge"], p["na_radius"]
+    assert (Np, L, r, len(x0)) == (256, 1024, 84, 193)
+    order = np.arange(len(x0))
+    B = 64
+    stack, idx = _tiled_stack(Np, L, r, x0, y0, B, 5, seed=212)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=B)
+    with fpm_amd.Solver(prob) as s:
+        info = s.info()
+        assert info.path == fpm_amd.PATH_GENERAL and info.fused_kernel == fpm_amd.KERNEL_GENERAL
+        assert info.box == 169
+        s.upload(stack)
+        s.init()
+        s.run(2)
+        out = s.download(objF=False, support=False)
+    sample = (0, 31, 63)
+    assert len({int(idx[b]) for b in sample}) == 3
+    refs = oracle_lib.run_fpm_batch(stack[:, sample], order, x0, y0, Np, L, r, p["delta1"], p["delta2"], 2,
+                                    threads=3, pupil=True)
+    for i, b in enumerate(sample):
+        for k in ("objCrop", "pupil"):
+            e = rel_l2(out[k][b], refs[k][i])
+            print(f"config2 at Np 256 (r 84) patch {b} {k} rel L2 {e:.2e}")
+            assert e < 5e-5, (k, b, e)
+
+
 def test_config3_dogstomach_literal_256_patches():
     """Config 3 as dataset_dogStomach.json states it: 157 LEDs (maxNA 0.4) in
     the reference's own unstable std::sort order, Np 200 / L 600 / r 26,

@@ -2,6 +2,7 @@
 # build a variant of libfpm_hip.so with extra compile flags into
 # fpm-opencv_amd/lib_<name>/ (same-box A/B runs load it via FPM_HIP_LIB)
 #   tools/build_var.sh <name> "<HIPFLAGS_EXTRA>" [git ref: build that commit's sources]
+#   MAKEVARS="MMC_FILES='np1024 objcrop'" tools/build_var.sh ...: extra make variables
 set -e
 name=$1; flags=$2; ref=$3
 root=$(cd "$(dirname "$0")/.." && pwd)
@@ -13,7 +14,7 @@ if [ -n "$ref" ]; then
 else
   cp -r $root/fpm-opencv_amd/csrc $root/fpm-opencv_amd/Makefile $tmp/fpm-opencv_amd/
 fi
-make -s -C $tmp/fpm-opencv_amd -j8 lib/libfpm_hip.so HIPFLAGS_EXTRA="$flags"
+eval make -s -C $tmp/fpm-opencv_amd -j8 lib/libfpm_hip.so HIPFLAGS_EXTRA=\"$flags\" ${MAKEVARS:-}
 mkdir -p $root/fpm-opencv_amd/lib_$name
 cp $tmp/fpm-opencv_amd/lib/libfpm_hip.so $root/fpm-opencv_amd/lib_$name/
 echo "built fpm-opencv_amd/lib_$name/libfpm_hip.so ($flags)"

@@ -29,7 +29,7 @@ def src_hash(csrc: str = CSRC) -> str:
     if os.path.isfile(mk):
         with open(mk, "rb") as f:
             for line in f.read().split(b"\n"):
-                if b"HIPFLAGS" in line or b"amdgpu-" in line:
+                if b"HIPFLAGS" in line or b"amdgpu-" in line or b"MMC_FILES" in line:
                     h.update(line)
     return h.hexdigest()[:16]
 
