@@ -65,7 +65,7 @@ size_t fused_dist_elems(int B, int ks);
 int fused_dist_parts(int B, int n_cu, int r, int L);
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, int stall_led, hipStream_t s);
+                             float2 *area, int *flags, int stall_led, unsigned tag_base, hipStream_t s);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 bool meas_layout_copy(const uint16_t *src, uint16_t *dst, int np, int g, size_t nimg, hipStream_t s,
@@ -192,6 +192,7 @@ struct fpm_ctx {
     float2 *xch = nullptr;          //   exchange area
     int *split_flags = nullptr;     //   handoff flags [KS B] + sticky abort flag + XCC ids [KS B]
     int stall_led = -1;             //   fpm_debug_set_stall (tests): the last part stops publishing
+    unsigned dist_tags = 0;         //   distributed mode: LEDs launched so far (tile-word tags)
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
@@ -478,6 +479,9 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         if (c->split_ks > 1) {
             const size_t nx = c->dist ? fused_dist_elems(B, c->split_ks) : fused_xch_elems(B, c->split_ks);
             if ((rc = dalloc(c, &c->xch, nx))) return fail(rc);
+            // distributed mode's tile words start at tag 0, which no LED uses
+            if (hipMemset(c->xch, 0, nx * sizeof(float2)) != hipSuccess)
+                return fail(set_err(FPM_ERR_DEVICE, "memset failed"));
             const size_t nf = fused_flag_words(B, c->split_ks);
             if ((rc = dalloc(c, &c->split_flags, nf))) return fail(rc);
             if (hipMemset(c->split_flags, 0, nf * sizeof(int)) != hipSuccess)
@@ -774,7 +778,9 @@ int fpm_run(fpm_ctx *c, int iters) {
                                               c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED && c->dist) {
             HIP_TRY(launch_fused_dist(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev, c->prob.n_order, c->tw_np,
-                                      c->split_ks, c->dbg, c->xch, c->split_flags, c->stall_led, c->stream));
+                                      c->split_ks, c->dbg, c->xch, c->split_flags, c->stall_led, c->dist_tags,
+                                      c->stream));
+            c->dist_tags = (c->dist_tags + (unsigned)c->prob.n_order) & 0x7fffffffu;
         } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->split_ks, c->dbg, c->xch,

@@ -49,6 +49,9 @@ struct FusedArgs {
     int ledtab_off;             // byte offset of the LED table in dynamic LDS (ledtab.hpp), or -1
     int stall_led;              // fpm_debug_set_stall (tests only): the last part stops
                                 // publishing from this LED on, forcing the timeout path; -1 off
+    unsigned tag_base;          // distributed mode: LEDs of the context's earlier launches, so
+                                // LED it of this launch tags its tile words tag_base + it + 1
+                                // (mod 2^31) and a word left by an earlier launch never matches
 };
 
 // split-mode exchange area per patch (float2): each part's F partials of the

@@ -24,13 +24,15 @@
 //            support columns -> F complete, no partial sums               (:394)
 //   update   object update of the own rows on the support (:405-447), pupil
 //            numerator (:457-464), tile maxima of |spec| in LDS
-//   sync 3   (carries the window's tile maxima / dirty bits)
+//   sync 3   the window's tile maxima / dirty bits as tagged words: the
+//            words themselves are the handoff (no flag)
 //   merge    every part folds the partners' window tiles into its LDS copy,
 //            so all parts hold identical tile maxima
 //   max      exact max|objF| (:460,467), redundant in every part (identical)
 //   P        P += num / max|objF| on the own rows (:468-475), max|P| partial
 //
-// Handoffs: one monotone flag per part (3 per LED); Tg, the tile
+// Handoffs: one monotone flag per part for syncs 1 and 2, tagged tile words
+// for sync 3 (the tag counts LEDs across launches, FusedArgs::tag_base); Tg, the tile
 // publications and the spectrum move with device-coherent policies (plain
 // stores + L1-bypassing loads when every part of the patch sits on one XCD --
 // the L2 is the coherence point -- sc1 otherwise), see fused_sync.hpp.
@@ -550,65 +552,92 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             cst(rs, wb0 + tp.x * L + tp.y, nv);
             note(yc + tp.x, xc + tp.y, oa, cmag(nv));
         }
-        __syncthreads();  // tile maxima of this part's pixels
-        // publish the window's tiles (the only ones any part changed)
+        // ---- sync 3 as tagged tile words (round 6).  Every wave's spectrum
+        // stores are acknowledged before the barrier, so once a part's window
+        // tile words carry this LED's tag its spectrum writes are visible: the
+        // words are the handoff.  The merge wave publishes this part's words
+        // and polls the partners' until every tag matches, holding the values
+        // it needs for the merge -- no flag store behind a second
+        // acknowledgement, no data load behind the flag.
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's spectrum stores acknowledged
+        __syncthreads();  // tile maxima of this part's pixels; every wave's stores acknowledged
+        FPM_STAMP(6)
         const int wnx = wtx1 - wtx0 + 1, wnt = wnx * (wty1 - wty0 + 1);
         auto wtile = [&](int k) {  // band index of window tile k
             const int dy = k / wnx;
             return (wty0 + dy - a.bty0) * a.nbx + (wtx0 + k - dy * wnx - a.btx0);
         };
-        // window tiles: thread ti handles tile ti (see towner)
-        if (ti < wnt) {
-            const int bk = wtile(ti);
-            cst(ra, TILES_OFF + hown * kWinTiles + ti,
-                make_float2(tmx[bk], __uint_as_float((dirty[bk >> 5] >> (bk & 31)) & 1u)));
-        }
-        FPM_STAMP(6)
-#ifdef FPM_DIST_SUBSTAMP
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's spectrum / tile stores acknowledged
-        FPM_STAMP(12)
-#endif
-        if (!handoff(nothing)) {  // ---- sync 3
-            aborted = true;
-            break;
-        }
-        FPM_STAMP(7)
-        // the next window first (its loads overlap the merge), then the
-        // merge: every part ends with the same maxima and dirty bits
-        if (it + 1 < a.n_order) load_window(it + 1);  // partners' spectrum writes are visible
-        float wcm = 0.f;      // merged window tile of this thread (ti < wnt)
-        bool wdirty = false;
-        if (ti < wnt) {
-            const int bk = wtile(ti);
-            // every partner's tile is loaded before the first is used: one L2
-            // round trip (the load-use loop waited for each in turn, KS - 1
-            // round trips)
+        if (w == WMERGE) {
+            // thread ti < wnt owns window tile ti (see towner: ti spans 0..63
+            // over this wave); the lane with ti == kWinTiles - 1 (never a
+            // tile: wnt <= 36) watches the abort word
+            const bool mine = ti < wnt, watch = ti == kWinTiles - 1;
+            const int bk = mine ? wtile(ti) : 0;
+            const float own = mine ? tmx[bk] : 0.f;
+            const unsigned odirty = mine ? (dirty[bk >> 5] >> (bk & 31)) & 1u : 0u;
+            const unsigned tag = (a.tag_base + (unsigned)it + 1u) & 0x7fffffffu;
+            // fault injection (fpm_debug_set_stall) as for the flags
+            const bool publish = a.stall_led < 0 || it < a.stall_led || hown != KS - 1;
+            if (mine && publish) cst(ra, TILES_OFF + hown * kWinTiles + ti, make_float2(own, __uint_as_float(tag << 1 | odirty)));
             float2 e[KS - 1];
+            bool ok = true;
+            for (int spins = 0;; ++spins) {
+                // every partner word of this lane's tile in one round trip
+                // (lane part of the offset in one VGPR, the partner's block
+                // offset in the scalar soffset: no per-partner address held
+                // across the LED loop)
 #pragma unroll
-            for (int q = 0; q < KS - 1; ++q) e[q] = cld(ra, TILES_OFF + (q < hown ? q : q + 1) * kWinTiles + ti);
-            float m = tmx[bk];
+                for (int q = 0; q < KS - 1; ++q)
+                    e[q] = mine ? __builtin_bit_cast(
+                                      float2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                  ra, ti * (int)sizeof(float2),
+                                                  (TILES_OFF + (q < hown ? q : q + 1) * kWinTiles) * (int)sizeof(float2),
+                                                  kAuxL2Volatile))
+                                : make_float2(0.f, 0.f);
+                const int ab = watch ? __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                bool done = true;
+#pragma unroll
+                for (int q = 0; q < KS - 1; ++q) done = done && (!mine || (__float_as_uint(e[q].y) >> 1) == tag);
+                if (__all(done)) break;
+                if (__any(ab != 0) || spins > (1 << 23)) {
+                    if (watch) __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            FPM_STAMP(7)
+            // merge: every part ends with the same maxima and dirty bits
+            float m = own;
             unsigned d = 0;
 #pragma unroll
             for (int q = 0; q < KS - 1; ++q) {
                 m = fmaxf(m, e[q].x);
-                d |= __float_as_uint(e[q].y);
+                d |= __float_as_uint(e[q].y) & 1u;
             }
-            tmx[bk] = m;
-            if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
-            wcm = m;
-            wdirty = d || ((dirty[bk >> 5] >> (bk & 31)) & 1u);
-        }
-        // the merge wave folds the window tiles into the outside maxima
-        if (w == WMERGE) {
-            float c = wdirty ? 0.f : wcm, d = wdirty ? wcm : 0.f;
+            if (mine) {
+                tmx[bk] = m;
+                if (d) atomicOr(&dirty[bk >> 5], 1u << (bk & 31));
+            }
+            const bool wdirty = (d | odirty) != 0;
+            // fold the window tiles into the outside maxima of sync 1
+            float c = mine && !wdirty ? m : 0.f, dd = mine && wdirty ? m : 0.f;
             c = wave_max_nonneg(c);
-            d = wave_max_nonneg(d);
+            dd = wave_max_nonneg(dd);
             if (lane == 0) {
                 red[0] = fmaxf(c, __uint_as_float(omx[0]));
-                red[16] = fmaxf(d, __uint_as_float(omx[1]));
+                red[16] = fmaxf(dd, __uint_as_float(omx[1]));
+                ccnt[1] = ok;
             }
         }
         __syncthreads();
+        if (!ccnt[1]) {
+            aborted = true;
+            break;
+        }
+        // the next window: partners' spectrum writes are visible; its loads
+        // are consumed at the next LED's gather, behind the max and P phases
+        if (it + 1 < a.n_order) load_window(it + 1);
         FPM_STAMP(8)
 
         // ---- exact max|objF| (:460,467), identical in every part: the
@@ -734,7 +763,7 @@ int fused_dist_parts(int B, int n_cu, int r, int L) {
 
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, int stall_led, hipStream_t s) {
+                             float2 *area, int *flags, int stall_led, unsigned tag_base, hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
     if (!g.ok || (ks != 2 && ks != 4 && ks != 8) || !area || !flags) return hipErrorInvalidValue;
     if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
@@ -775,6 +804,7 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     a.flags = flags;
     a.abort_flag = flags + ks * st.B;
     a.stall_led = stall_led;
+    a.tag_base = tag_base;
     const size_t lds0 = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
     if (lds0 > 160 * 1024) return hipErrorInvalidValue;
     size_t lds;  // + the LED table when it fits
