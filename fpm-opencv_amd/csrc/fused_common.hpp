@@ -61,7 +61,12 @@ struct FusedArgs {
 constexpr int kXchTF = 12 * 512, kXchHalf = kXchTF + 64;
 constexpr int xch_patch_elems(int ks) { return 2 * ks * kXchHalf; }
 
-__device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * fz::SK[s] - (s >= 3 ? fz::NP : 0); }
+// kx of slot s of lane t: t + 16 SK[s] - (s >= 3 ? Np : 0), written without
+// the table (SK[s] = s + 10 [s >= 3]) so a run-time s (the spread object
+// update) is arithmetic, not a global load whose wait drains every
+// outstanding memory operation
+__device__ __forceinline__ int slot_kx(int t, int s) { return t + 16 * s - (s >= 3 ? 96 : 0); }
+static_assert(fz::SK[3] * 16 - fz::NP == 3 * 16 - 96 && fz::SK[5] * 16 - fz::NP == 5 * 16 - 96, "slot_kx");
 
 // ------------------------------------------------------------------ host side
 struct FusedGeom {

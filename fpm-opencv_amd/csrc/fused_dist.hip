@@ -69,6 +69,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     static_assert(KS == 2 || KS == 4 || KS == 8, "two, four or eight parts");
     ClockProbe probe;
     probe.start();
+    // measurement prefetch (KS 4 / 8; at KS 2 the part's 64 KB do not fit)
+    constexpr bool kPrefI = KS >= 4;
+    constexpr int NCH = TH * 512 / 1024;  // 1 KB wave-instruction chunks of the part's measurement
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
     float2 *scr_all = sm;                           // NG * XTILE exchange tiles
@@ -84,6 +87,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     float *tmx = (float *)(tpq + MAXTAIL);          // nbt: max|spec| per band tile (upper bound if dirty)
     unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits
     int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // [0] pass-B block counter, [1] handoff result
+    // KS 4 / 8: the LED's measurement for this part's columns, TH x 512 bytes
+    // in the column layout, copied into LDS by LDS-DMA one LED ahead
+    uint4 *mI = (uint4 *)((char *)sm + ((((char *)(ccnt + 2) - (char *)sm) + 15) & ~15));
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
@@ -163,9 +169,10 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
     // the launch's LED order as an LDS table (ledtab.hpp)
-    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
-    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
-    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
+    const bool lton = a.ledtab_off >= 0;
+    int2 *ltl = (int2 *)((char *)sm + (lton ? a.ledtab_off : 0));  // an LDS pointer either way (ledtab.hpp)
+    const LedTab lt{ltl, lton, a.order, a.x0, a.y0, NP / 2};
+    if (lton) lt.fill(ltl, a.n_order, tid, NT);
     __syncthreads();  // tpx / tpq / sig; LED table
     const int zoff = nrows * TLD;
     int roff[6];
@@ -271,6 +278,36 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (towner) Ot = cld(rs, wbase(itn) + tp.x * L + tp.y);
     };
     if (a.n_order > 0) load_window(0);
+    // The measurement of LED `itn` for this part's columns [TH hown, TH hown +
+    // TH): TH x 512 contiguous bytes of the column layout (meas_layout g = 16),
+    // copied linearly into mI by LDS-DMA (global_load_lds_dwordx4: no VGPRs,
+    // each wave its 1 KB chunks).  Issued at the start of pass A (pass B of
+    // the previous LED read the buffer two handoffs earlier), retired by the
+    // explicit s_waitcnt(0) of sync 1's publish, before the barrier after
+    // which pass B reads mI: the HBM latency runs under pass A (arithmetic
+    // and LDS only) instead of inside pass B's column chain.
+    // Only with the LED table in LDS: its LED index is read straight from
+    // there (LedTab::at's global fallback made the compiler select between
+    // the two tables and issue a flat load, whose wait drained the copy).
+    // The DMA is issued from inline asm: hipcc tracks its own LDS-DMA builtin
+    // and then waits vmcnt(0) before any LDS read it cannot prove disjoint
+    // from the destination, or at the next scratch reload; hipcc does not
+    // count an asm load, so its counted waits can only over-wait.
+    const bool pref = kPrefI && lton;
+    const unsigned mI_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)mI);
+    auto prefetch_I = [&](int itn) {
+        const char *src = (const char *)(a.meas + ((size_t)ltl[itn].x * st.B + b) * NP * NP) + TH * hown * 512;
+        for (int k = w; k < NCH; k += NW) {  // wave-uniform
+            const unsigned dst = __builtin_amdgcn_readfirstlane(mI_lds + (unsigned)k * 1024u);
+            const char *gsrc = src + k * 1024 + lane * 16;
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                         "s_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(gsrc), "s"(dst)
+                         : "memory");
+        }
+    };
     const float epsn = st.eps * (float)(NP * NP);
     const float epsn_im = st.eps_im * (float)(NP * NP);
     unsigned *tmu = (unsigned *)tmx;
@@ -290,11 +327,18 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (tid == 0) omx[0] = omx[1] = 0u;  // read by the previous LED's merge, two barriers ago
         __syncthreads();  // tailX
         FPM_STAMP(0)
+        // X = O P first (its loads are then waited for), the measurement DMA
+        // next: pass A is pure arithmetic and LDS up to sync 1's
+        // acknowledgement wait, which retires the copy
+        float2 X6[6];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) X6[s] = g < NOWN ? pout(pmul(pin(Opre[s]), pin(P[s]))) : make_float2(0.f, 0.f);  // :364
+        if (pref) prefetch_I(it);
         if (g < NOWN) {  // group-uniform
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
+            for (int s = 0; s < 6; ++s) v[SK[s]] = X6[s];
             idft256_in6(v, r, scr, wt, t, xrd);
             if (ron) {
 #pragma unroll
@@ -390,9 +434,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         {
             auto colx = [&](int r8) { return (r8 % CB) + CB * gg + 4 * CB * (r8 / CB); };
             auto ldI = [&](int xl, uint4 (&n)[2]) {
-                const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * hown) * 16 + t) * 16);
+                if (pref) {  // the LDS copy: lane t's 32 bytes of column xl
 #pragma unroll
-                for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
+                    for (int i = 0; i < 2; ++i) n[i] = mI[(xl * 16 + t) * 2 + i];
+                } else {
+                    const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * hown) * 16 + t) * 16);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
+                }
             };
             float2 tin[6];
 #pragma unroll
@@ -733,9 +782,12 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 // ------------------------------------------------------------------ host side
 size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
     const int tld = fz::NP / ks + 1;
-    return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
-           48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
-           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
+    const size_t base = (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) *
+                            sizeof(float2) +
+                        48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
+                        (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
+    // + the KS 4 / 8 measurement buffer mI, 16-byte aligned
+    return ks >= 4 ? ((base + 15) & ~(size_t)15) + (size_t)(fz::NP / ks) * 512 : base;
 }
 
 // distributed-mode area (float2 elements) for B patches
