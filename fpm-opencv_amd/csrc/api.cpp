@@ -65,8 +65,7 @@ size_t fused_dist_elems(int B, int ks);
 int fused_dist_parts(int B, int n_cu, int r, int L);
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, int stall_led, unsigned tag_base, unsigned sync_base,
-                             hipStream_t s);
+                             float2 *area, int *flags, int stall_led, unsigned tag_base, hipStream_t s);
 // in-place measurement layout of the fused kernels (preprocess.hip)
 hipError_t meas_layout(uint16_t *meas, int np, int g, size_t nimg, bool fwd, hipStream_t s);
 bool meas_layout_copy(const uint16_t *src, uint16_t *dst, int np, int g, size_t nimg, hipStream_t s,
@@ -194,7 +193,6 @@ struct fpm_ctx {
     int *split_flags = nullptr;     //   handoff flags [KS B] + sticky abort flag + XCC ids [KS B]
     int stall_led = -1;             //   fpm_debug_set_stall (tests): the last part stops publishing
     unsigned dist_tags = 0;         //   distributed mode: LEDs launched so far (tile-word tags)
-    unsigned dist_syncs = 0;        //   distributed mode: handoffs launched so far (per-wave flags)
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
@@ -781,10 +779,8 @@ int fpm_run(fpm_ctx *c, int iters) {
         } else if (c->path == FPM_PATH_FUSED && c->dist) {
             HIP_TRY(launch_fused_dist(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev, c->prob.n_order, c->tw_np,
                                       c->split_ks, c->dbg, c->xch, c->split_flags, c->stall_led, c->dist_tags,
-                                      c->dist_syncs, c->stream));
+                                      c->stream));
             c->dist_tags = (c->dist_tags + (unsigned)c->prob.n_order) & 0x7fffffffu;
-            // two flagged handoffs per LED and the final one (fused_dist.hip)
-            c->dist_syncs = (c->dist_syncs + 2u * (unsigned)c->prob.n_order + 1u) & 0x7fffffffu;
         } else if (c->path == FPM_PATH_FUSED) {
             HIP_TRY(launch_fused_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                            c->prob.n_order, c->tw_np, c->split_ks, c->dbg, c->xch,

@@ -52,8 +52,6 @@ struct FusedArgs {
     unsigned tag_base;          // distributed mode: LEDs of the context's earlier launches, so
                                 // LED it of this launch tags its tile words tag_base + it + 1
                                 // (mod 2^31) and a word left by an earlier launch never matches
-    unsigned sync_base;         // distributed mode: handoffs of the context's earlier launches
-                                // (per-wave flag values go on counting, mod 2^31)
 };
 
 // split-mode exchange area per patch (float2): each part's F partials of the

@@ -31,9 +31,8 @@
 //   max      exact max|objF| (:460,467), redundant in every part (identical)
 //   P        P += num / max|objF| on the own rows (:468-475), max|P| partial
 //
-// Handoffs: one flag per wave for syncs 1 and 2, tagged tile words for sync
-// 3 (flag values and tags count across launches, FusedArgs::sync_base /
-// tag_base, so nothing is reset per launch); Tg, the tile
+// Handoffs: one monotone flag per part for syncs 1 and 2, tagged tile words
+// for sync 3 (the tag counts LEDs across launches, FusedArgs::tag_base); Tg, the tile
 // publications and the spectrum move with device-coherent policies (plain
 // stores + L1-bypassing loads when every part of the patch sits on one XCD --
 // the L2 is the coherence point -- sc1 otherwise), see fused_sync.hpp.
@@ -56,10 +55,7 @@ constexpr int kTgRows = fz::NROWS + fz::MAXTAILROWS;  // Tg rows: 64 FFT rows + 
 constexpr int kWinTiles = 64;                         // window tiles published per part (<= 6 x 6 used)
 // per-patch distributed-mode area (float2): Tg, then KS x kWinTiles tile
 // publications (max, dirty flag), then KS max|P| partials
-// + the per-wave handoff flags, ks x 8 ints (ks x 4 float2)
-constexpr size_t dist_patch_elems(int ks) {
-    return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + ks + (size_t)ks * 4;
-}
+constexpr size_t dist_patch_elems(int ks) { return (size_t)kTgRows * fz::NP + (size_t)ks * kWinTiles + ks; }
 }  // namespace
 
 template <int KS>
@@ -73,9 +69,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     static_assert(KS == 2 || KS == 4 || KS == 8, "two, four or eight parts");
     ClockProbe probe;
     probe.start();
-    // measurement prefetch (KS 4 / 8; at KS 2 the part's 64 KB do not fit)
-    constexpr bool kPrefI = KS >= 4;
-    constexpr int NCH = TH * 512 / 1024;  // 1 KB wave-instruction chunks of the part's measurement
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int nrows = NROWS + a.n_tail_rows;
     float2 *scr_all = sm;                           // NG * XTILE exchange tiles
@@ -91,9 +84,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     float *tmx = (float *)(tpq + MAXTAIL);          // nbt: max|spec| per band tile (upper bound if dirty)
     unsigned *dirty = (unsigned *)(tmx + a.nbt);    // nbt bits
     int *ccnt = (int *)(dirty + ((a.nbt + 31) >> 5));  // [0] pass-B block counter, [1] handoff result
-    // KS 4 / 8: the LED's measurement for this part's columns, TH x 512 bytes
-    // in the column layout, copied into LDS by LDS-DMA one LED ahead
-    uint4 *mI = (uint4 *)((char *)sm + ((((char *)(ccnt + 2) - (char *)sm) + 15) & ~15));
 
     const DevState &st = a.st;
     const int tid = threadIdx.x, g = tid >> 4, t = tid & 15, gg = (tid >> 4) & 3;
@@ -105,6 +95,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     const int b = (int)((blockIdx.x / (8 * KS)) * 8 + (blockIdx.x & 7));
     if (b >= st.B) return;  // grid rounded up to 8 KS blocks (block-uniform)
     float2 *area = a.xch + (size_t)b * dist_patch_elems(KS);
+    int *flg = a.flags + KS * b;
     int *xccs = a.flags + KS * st.B + 1 + KS * b;
     const int R = st.r, NB = st.nb, L = st.L;
     float2 *scr = scr_all + g * XTILE;
@@ -118,7 +109,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     static_assert(!kSpreadUpd || 3 * NOWN * 96 <= (NG - NOWN) * XTILE, "staging fits the idle groups' tiles");
     float2 *upd_f = scr_all + NOWN * XTILE, *upd_o = upd_f + NOWN * 96, *upd_p = upd_o + NOWN * 96;
     constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
-    constexpr int WFLG_OFF = 2 * (PMX_OFF + KS);  // int index of the per-wave flags [KS][NW]
 
     // ---- one-time setup
     if (tid == 0) {
@@ -228,6 +218,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     const __amdgpu_buffer_rsrc_t ra =
         __builtin_amdgcn_make_buffer_rsrc(area, 0, (int)(dist_patch_elems(KS) * sizeof(float2)), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(spec, 0, L * L * (int)sizeof(float2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(flg, 0, KS * (int)sizeof(int), 0x00020000);
     // partner-visible loads / stores: every load L1-bypassing (sc1, served by
     // the L2 or memory); stores plain inside one XCD (the line stays in the
     // shared L2), device-scope write-through (sc1) across XCDs
@@ -240,59 +231,18 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (local) __builtin_amdgcn_raw_buffer_store_b64(d, r, off, 0, 0);
         else __builtin_amdgcn_raw_buffer_store_b64(d, r, off, 0, 16);
     };
-    int sync_no = 0;  // handoffs of this launch
+    int sync_no = 0;  // handoffs of this launch (flag values are 1, 2, 3, ...)
     bool aborted = false;
     int cur = 0;      // LED position of the handoffs below
     // idle(): work for waves 1 .. NW-1 while the first wave polls the
     // partners' flags (this part's flag is already out)
-    // Syncs 1 and 2 (and the final one) with one flag per WAVE (round 6): a
-    // wave publishes as soon as its own stores are acknowledged -- no block
-    // barrier before a single flag store -- and lane l of the first wave
-    // polls partner wave flag l (56 at KS 8, one vector load per spin).  The
-    // values count handoffs across launches (sync_base), so the flags are
-    // never reset; the wait compares with a wrap-safe signed difference.
     auto handoff = [&](auto &&idle) {
         ++sync_no;
-        const int val = (int)((a.sync_base + (unsigned)sync_no) & 0x7fffffffu);
-        if (a.stall_led < 0 || cur < a.stall_led || hown != KS - 1) {
-            __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged
-            if (lane == 0) {
-                const int off = (WFLG_OFF + hown * NW + w) * (int)sizeof(int);
-                if (local) __builtin_amdgcn_raw_buffer_store_b32((unsigned)val, ra, off, 0, 0);
-                else __builtin_amdgcn_raw_buffer_store_b32((unsigned)val, ra, off, 0, 16);
-            }
-        }
+        // fault injection (fpm_debug_set_stall): the last part stops
+        // publishing from LED position stall_led on, its partners time out
+        if (a.stall_led < 0 || cur < a.stall_led || hown != KS - 1) handoff_publish(flg + hown, sync_no, local);
         if (w > 0) idle();
-        if (w == 0) {
-            constexpr int NPOLL = (KS - 1) * NW;
-            static_assert(NPOLL < 64, "one polling lane per partner wave, lane 63 watches the abort word");
-            const int q = lane / NW, pw = lane - q * NW;
-            const int flagi = WFLG_OFF + (q < hown ? q : q + 1) * NW + pw;
-            const bool poll = lane < NPOLL, watch = lane == 63;
-            bool done = !poll;
-            int ok = 1;
-            for (int spins = 0;; ++spins) {
-                int f = 0;
-                if (poll && !done) f = ld_l2_i32(ra, flagi * (int)sizeof(int));
-                else if (watch) f = __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (poll) done = done || (f - val) >= 0;
-                const bool ab = __builtin_amdgcn_readlane(watch ? f : 0, 63) != 0;
-                if (__all(done)) break;
-                if (ab) {
-                    ok = 0;
-                    break;
-                }
-                if (spins > (1 << 23)) {
-                    if (lane == 0) __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (lane == 0) ccnt[1] = ok;
-        }
-        __syncthreads();
-        return ccnt[1] != 0;
+        return handoff_wait<KS>(flg, hown, sync_no, a.abort_flag, ccnt + 1, local, rf);
     };
     auto nothing = []() {};
     // exact max|objF| (:460,467): the window's tiles are merged on one wave
@@ -322,36 +272,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (towner) Ot = cld(rs, wbase(itn) + tp.x * L + tp.y);
     };
     if (a.n_order > 0) load_window(0);
-    // The measurement of LED `itn` for this part's columns [TH hown, TH hown +
-    // TH): TH x 512 contiguous bytes of the column layout (meas_layout g = 16),
-    // copied linearly into mI by LDS-DMA (global_load_lds_dwordx4: no VGPRs,
-    // each wave its 1 KB chunks).  Issued at the start of pass A (pass B of
-    // the previous LED read the buffer two handoffs earlier), retired by the
-    // explicit s_waitcnt(0) of sync 1's publish, before the barrier after
-    // which pass B reads mI: the HBM latency runs under pass A (arithmetic
-    // and LDS only) instead of inside pass B's column chain.
-    // Only with the LED table in LDS: its LED index is read straight from
-    // there (LedTab::at's global fallback made the compiler select between
-    // the two tables and issue a flat load, whose wait drained the copy).
-    // The DMA is issued from inline asm: hipcc tracks its own LDS-DMA builtin
-    // and then waits vmcnt(0) before any LDS read it cannot prove disjoint
-    // from the destination, or at the next scratch reload; hipcc does not
-    // count an asm load, so its counted waits can only over-wait.
-    const bool pref = kPrefI && lton;
-    const unsigned mI_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)mI);
-    auto prefetch_I = [&](int itn) {
-        const char *src = (const char *)(a.meas + ((size_t)ltl[itn].x * st.B + b) * NP * NP) + TH * hown * 512;
-        for (int k = w; k < NCH; k += NW) {  // wave-uniform
-            const unsigned dst = __builtin_amdgcn_readfirstlane(mI_lds + (unsigned)k * 1024u);
-            const char *gsrc = src + k * 1024 + lane * 16;
-            unsigned keep;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
-                         "s_mov_b32 m0, %0"
-                         : "=&s"(keep)
-                         : "v"(gsrc), "s"(dst)
-                         : "memory");
-        }
-    };
     const float epsn = st.eps * (float)(NP * NP);
     const float epsn_im = st.eps_im * (float)(NP * NP);
     unsigned *tmu = (unsigned *)tmx;
@@ -371,18 +291,11 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (tid == 0) omx[0] = omx[1] = 0u;  // read by the previous LED's merge, two barriers ago
         __syncthreads();  // tailX
         FPM_STAMP(0)
-        // X = O P first (its loads are then waited for), the measurement DMA
-        // next: pass A is pure arithmetic and LDS up to sync 1's
-        // acknowledgement wait, which retires the copy
-        float2 X6[6];
-#pragma unroll
-        for (int s = 0; s < 6; ++s) X6[s] = g < NOWN ? pout(pmul(pin(Opre[s]), pin(P[s]))) : make_float2(0.f, 0.f);  // :364
-        if (pref) prefetch_I(it);
         if (g < NOWN) {  // group-uniform
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int s = 0; s < 6; ++s) v[SK[s]] = X6[s];
+            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
             idft256_in6(v, r, scr, wt, t, xrd);
             if (ron) {
 #pragma unroll
@@ -478,14 +391,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         {
             auto colx = [&](int r8) { return (r8 % CB) + CB * gg + 4 * CB * (r8 / CB); };
             auto ldI = [&](int xl, uint4 (&n)[2]) {
-                if (pref) {  // the LDS copy: lane t's 32 bytes of column xl
+                const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * hown) * 16 + t) * 16);
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) n[i] = mI[(xl * 16 + t) * 2 + i];
-                } else {
-                    const uint4 *ip = (const uint4 *)(Ib + ((xl + TH * hown) * 16 + t) * 16);
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
-                }
+                for (int i = 0; i < 2; ++i) n[i] = ld_stream(ip + i);
             };
             float2 tin[6];
 #pragma unroll
@@ -826,12 +734,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 // ------------------------------------------------------------------ host side
 size_t fused_dist_lds_bytes(int ks, int nbt, int n_tail_rows) {
     const int tld = fz::NP / ks + 1;
-    const size_t base = (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) *
-                            sizeof(float2) +
-                        48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
-                        (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
-    // + the KS 4 / 8 measurement buffer mI, 16-byte aligned
-    return ks >= 4 ? ((base + 15) & ~(size_t)15) + (size_t)(fz::NP / ks) * 512 : base;
+    return (size_t)(32 * XTILE + (fz::NROWS + n_tail_rows + 2) * tld + 512 + 2 * fz::MAXTAIL) * sizeof(float2) +
+           48 * sizeof(float) + 96 * sizeof(int) + fz::MAXTAIL * (sizeof(int2) + sizeof(int)) +
+           (size_t)nbt * sizeof(float) + (size_t)(nbt + 31) / 32 * sizeof(unsigned) + 2 * sizeof(int);
 }
 
 // distributed-mode area (float2 elements) for B patches
@@ -859,8 +764,7 @@ int fused_dist_parts(int B, int n_cu, int r, int L) {
 
 hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int *order_dev, const int *x0_dev,
                              const int *y0_dev, int n_order, const float2 *tw_np, int ks, unsigned long long *dbg,
-                             float2 *area, int *flags, int stall_led, unsigned tag_base, unsigned sync_base,
-                             hipStream_t s) {
+                             float2 *area, int *flags, int stall_led, unsigned tag_base, hipStream_t s) {
     const FusedGeom g = fused_geometry(st.np, st.r);
     if (!g.ok || (ks != 2 && ks != 4 && ks != 8) || !area || !flags) return hipErrorInvalidValue;
     if (st.sy0 < 0 || st.sy1 >= st.L || st.sy0 > st.sy1 || st.sx0 < 0 || st.sx1 >= st.L || st.sx0 > st.sx1)
@@ -902,7 +806,6 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
     a.abort_flag = flags + ks * st.B;
     a.stall_led = stall_led;
     a.tag_base = tag_base;
-    a.sync_base = sync_base;
     const size_t lds0 = fused_dist_lds_bytes(ks, a.nbt, g.n_tail_rows);
     if (lds0 > 160 * 1024) return hipErrorInvalidValue;
     size_t lds;  // + the LED table when it fits
@@ -912,9 +815,9 @@ hipError_t launch_fused_dist(const DevState &st, const uint16_t *meas, const int
                                : (const void *)k_fused_dist<2>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    // XCC ids restart at zero; the abort word is sticky; the per-wave flags
-    // (in the area) count on across launches (sync_base)
-    e = hipMemsetAsync(flags + ks * st.B + 1, 0, (size_t)ks * st.B * sizeof(int), s);
+    // handoff counters and XCC ids restart at zero; the abort word is sticky
+    e = hipMemsetAsync(flags, 0, (size_t)ks * st.B * sizeof(int), s);
+    if (e == hipSuccess) e = hipMemsetAsync(flags + ks * st.B + 1, 0, (size_t)ks * st.B * sizeof(int), s);
     if (e != hipSuccess) return e;
     return launch_coresident(fn, 8 * ks * ((st.B + 7) / 8), 512, lds, &a, s);
 }
