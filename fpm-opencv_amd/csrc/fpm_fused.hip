@@ -47,10 +47,6 @@
 
 namespace fpm {
 
-#ifndef FPM_BPRIO
-#define FPM_BPRIO 0  // A/B knob: s_setprio of a younger wave (w >= NW/2) for its last pass-B block
-#endif
-
 // Column parts: T (the row IDFTs of the box rows) is held in LDS one column
 // part at a time -- two halves of 128 columns walked in turn by the
 // one-workgroup kernel (KS = 1), or the one part a split-mode workgroup owns
@@ -441,7 +437,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 int nx = 0;
                 if (lane == 0) nx = atomicAdd(ccnt, 1);
                 nx = __builtin_amdgcn_readfirstlane(nx);
-                if (FPM_BPRIO && nx >= NBLK && w >= NW / 2) __builtin_amdgcn_s_setprio(FPM_BPRIO);
                 ldI(xl, cI);
 #pragma unroll
                 for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
@@ -475,7 +470,6 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
                 if (nx >= NBLK) break;
                 r8 = nx;
             }
-            if (FPM_BPRIO) __builtin_amdgcn_s_setprio(0);
             FPM_STAMP(10)  // this wave's own columns done
             __syncthreads();
             FPM_STAMP(2)

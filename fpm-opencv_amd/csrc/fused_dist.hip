@@ -699,7 +699,10 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 #undef FPM_STAMP
     __syncthreads();  // red[32..]
     probe.stop(a.st.clk);
-    if (a.dbg && tid == 0 && (hown == 0 || hown == KS - 1))
+#ifndef FPM_STAMP_PART2
+#define FPM_STAMP_PART2 (KS - 1)  // diagnostic builds: the part recorded in the second stamp slot
+#endif
+    if (a.dbg && tid == 0 && (hown == 0 || hown == FPM_STAMP_PART2))
         for (int i = 0; i < kStamps; ++i) atomicAdd(&a.dbg[(hown ? kStamps : 0) + i], acc[i]);
     // ---- write back: each part its own pupil rows and tail pixels; part 0
     // the tile maxima (identical in every part) and max|P| over all parts
