@@ -171,10 +171,9 @@ __global__ void __launch_bounds__(NT, 1) k_fused_iteration(FusedArgs a) {
         }
     }
     // the launch's LED order as an LDS table (ledtab.hpp)
-    const bool lton = a.ledtab_off >= 0;
-    int2 *ltl = (int2 *)((char *)sm + (lton ? a.ledtab_off : 0));  // an LDS pointer either way (ledtab.hpp)
-    const LedTab lt{ltl, lton, a.order, a.x0, a.y0, NP / 2};
-    if (lton) lt.fill(ltl, a.n_order, tid, NT);
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
     __syncthreads();  // tpx / tky / sig; LED table
     // per-lane half-T row offsets of this lane's six column slots; rows
     // outside the box read the zero row `nrows` and write the dummy row after it

@@ -163,10 +163,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
     // the launch's LED order as an LDS table (ledtab.hpp)
-    const bool lton = a.ledtab_off >= 0;
-    int2 *ltl = (int2 *)((char *)sm + (lton ? a.ledtab_off : 0));  // an LDS pointer either way (ledtab.hpp)
-    const LedTab lt{ltl, lton, a.order, a.x0, a.y0, NP / 2};
-    if (lton) lt.fill(ltl, a.n_order, tid, NT);
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
     __syncthreads();  // tpx / tpq / sig; LED table
     const int zoff = nrows * TLD;
     int roff[6];
@@ -480,8 +479,16 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // row; pixels go to the last groups first, which own no FFT row at
         // KS 4 / 8, so the sums overlap the row DFTs instead of following them
         // on the same groups (round 3: C 7.5k cycles per LED on the parts
-        // that own a tail row vs 3.2k on the part that owns none, at KS 4)
-        for (int pp = NG - 1 - g; pp < a.n_tail_px; pp += NG) {
+        // that own a tail row vs 3.2k on the part that owns none, at KS 4).
+        // At KS 8 the row DFTs run on waves 0 and 1 only (SIMDs 0 and 1), so
+        // the sums go to the 16 groups of waves 2, 3, 6 and 7 (SIMDs 2 and 3):
+        // on waves 4 and 5 they took issue slots from the row DFTs beside
+        // them -- the part owning the 17-pixel tail row ran C 0.6-0.8k cycles
+        // longer than the others, which waited for it at sync 3 (round 6,
+        // per-part stamps, profiles/r06_ab/dist_parts_pt128_c2c3_ab.txt)
+        constexpr int TSTRIDE = KS == 8 ? 16 : NG;
+        const int tslot = KS != 8 ? NG - 1 - g : (w == 2 || w == 3) ? 4 * (w - 2) + gg : (w >= 6) ? 8 + 4 * (w - 6) + gg : -1;
+        for (int pp = tslot; tslot >= 0 && pp < a.n_tail_px; pp += TSTRIDE) {
             if ((tpq[pp] % KS) != hown) continue;  // group-uniform
             const int2 px = tpx[pp];
             const int row = NROWS + tpq[pp];

@@ -164,10 +164,9 @@ __global__ void __launch_bounds__(fm::NT, 1) k_fused_mr(FusedMRArgs a) {
         P[s] = in ? pup[(kyr + R) * NB + kx + R] : make_float2(0.f, 0.f);
     }
     // the launch's LED order as an LDS table (ledtab.hpp)
-    const bool lton = a.ledtab_off >= 0;
-    int2 *ltl = (int2 *)((char *)sm + (lton ? a.ledtab_off : 0));  // an LDS pointer either way (ledtab.hpp)
-    const LedTab lt{ltl, lton, a.order, a.x0, a.y0, NP / 2};
-    if (lton) lt.fill(ltl, a.n_order, tid, NT);
+    int2 *ltl = a.ledtab_off >= 0 ? (int2 *)((char *)sm + a.ledtab_off) : nullptr;
+    const LedTab lt{ltl, a.order, a.x0, a.y0, NP / 2};
+    if (ltl) lt.fill(ltl, a.n_order, tid, NT);
     if (tid == 0) omx[0] = omx[1] = 0u;
     __syncthreads();  // sig, tw2
     // T row offsets of this lane's six column slots (zero row outside the box)

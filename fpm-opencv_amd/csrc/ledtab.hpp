@@ -18,12 +18,7 @@ struct LedPos {
 };
 
 struct LedTab {
-    // [n_order] {led, yc << 16 | xc}.  Always a pointer into the kernel's
-    // dynamic LDS (offset 0 when the table is off), never null: a pointer that
-    // may be null is a generic pointer, and each lookup then became a flat
-    // load whose s_waitcnt drained every outstanding global load and LDS-DMA
-    const int2 *lds;
-    bool on;          // the table is in LDS; else the global tables are read
+    const int2 *lds;  // [n_order] {led, yc << 16 | xc}, or null
     const int *order, *x0, *y0;
     int half;         // Np / 2
 
@@ -35,7 +30,7 @@ struct LedTab {
         }
     }
     __device__ __forceinline__ LedPos at(int it) const {
-        if (on) {
+        if (lds) {
             const int2 e = lds[it];
             // centres are in [0, L): unsigned 16-bit fields (ledtab_offset
             // refuses the table for L > 65536)
