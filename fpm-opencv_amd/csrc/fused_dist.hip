@@ -303,10 +303,12 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         // own tail rows: direct sums over the row's pixels for every column x,
         // on the LAST waves (the FFT-row groups g < NOWN sit in the first
-        // waves, so at KS 4 / 8 the sums run beside the row IDFTs)
+        // waves, so at KS 4 / 8 the sums run beside the row IDFTs); at KS 8
+        // on waves 2, 3, 6, 7 -- the SIMDs without a row-IDFT wave (see pass C)
+        const int tx = KS != 8 ? NT - 1 - tid : (w == 2 || w == 3) ? 64 * (w - 2) + lane : (w >= 6) ? 128 + 64 * (w - 6) + lane : NP;
         for (int q = hown; q < a.n_tail_rows; q += KS) {
             const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
-            for (int x = NT - 1 - tid; x < NP; x += NT) {
+            for (int x = tx; x < NP; x += NT) {
                 const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
                 pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
                 const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
