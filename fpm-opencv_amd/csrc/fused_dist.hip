@@ -105,7 +105,10 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     // update).  32-patch shard 2.74 -> 2.83 M (update 3.6k -> 2.2k cycles per
     // LED); at KS 4 (four owner waves) the staging stores in C cost what the
     // spread saved (64-patch shard 4.16 vs 4.10 M), profiles/r05_ab/dist_max_upd_ab.txt
-    constexpr bool kSpreadUpd = KS == 8;
+#ifndef FPM_SPREAD4
+#define FPM_SPREAD4 0  // A/B knob: the spread object update at KS 4 too
+#endif
+    constexpr bool kSpreadUpd = KS == 8 || (FPM_SPREAD4 && KS == 4);
     static_assert(!kSpreadUpd || 3 * NOWN * 96 <= (NG - NOWN) * XTILE, "staging fits the idle groups' tiles");
     float2 *upd_f = scr_all + NOWN * XTILE, *upd_o = upd_f + NOWN * 96, *upd_p = upd_o + NOWN * 96;
     constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
@@ -303,12 +306,10 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         }
         // own tail rows: direct sums over the row's pixels for every column x,
         // on the LAST waves (the FFT-row groups g < NOWN sit in the first
-        // waves, so at KS 4 / 8 the sums run beside the row IDFTs); at KS 8
-        // on waves 2, 3, 6, 7 -- the SIMDs without a row-IDFT wave (see pass C)
-        const int tx = KS != 8 ? NT - 1 - tid : (w == 2 || w == 3) ? 64 * (w - 2) + lane : (w >= 6) ? 128 + 64 * (w - 6) + lane : NP;
+        // waves, so at KS 4 / 8 the sums run beside the row IDFTs)
         for (int q = hown; q < a.n_tail_rows; q += KS) {
             const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
-            for (int x = tx; x < NP; x += NT) {
+            for (int x = NT - 1 - tid; x < NP; x += NT) {
                 const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
                 pf2 wa = pin(tw[ti]), wb = pin(tw[(ti + x) & (NP - 1)]);
                 const pf2 wstep = pin(tw[(2 * x) & (NP - 1)]);
@@ -481,16 +482,8 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // row; pixels go to the last groups first, which own no FFT row at
         // KS 4 / 8, so the sums overlap the row DFTs instead of following them
         // on the same groups (round 3: C 7.5k cycles per LED on the parts
-        // that own a tail row vs 3.2k on the part that owns none, at KS 4).
-        // At KS 8 the row DFTs run on waves 0 and 1 only (SIMDs 0 and 1), so
-        // the sums go to the 16 groups of waves 2, 3, 6 and 7 (SIMDs 2 and 3):
-        // on waves 4 and 5 they took issue slots from the row DFTs beside
-        // them -- the part owning the 17-pixel tail row ran C 0.6-0.8k cycles
-        // longer than the others, which waited for it at sync 3 (round 6,
-        // per-part stamps, profiles/r06_ab/dist_parts_pt128_c2c3_ab.txt)
-        constexpr int TSTRIDE = KS == 8 ? 16 : NG;
-        const int tslot = KS != 8 ? NG - 1 - g : (w == 2 || w == 3) ? 4 * (w - 2) + gg : (w >= 6) ? 8 + 4 * (w - 6) + gg : -1;
-        for (int pp = tslot; tslot >= 0 && pp < a.n_tail_px; pp += TSTRIDE) {
+        // that own a tail row vs 3.2k on the part that owns none, at KS 4)
+        for (int pp = NG - 1 - g; pp < a.n_tail_px; pp += NG) {
             if ((tpq[pp] % KS) != hown) continue;  // group-uniform
             const int2 px = tpx[pp];
             const int row = NROWS + tpq[pp];
