@@ -105,10 +105,9 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     // update).  32-patch shard 2.74 -> 2.83 M (update 3.6k -> 2.2k cycles per
     // LED); at KS 4 (four owner waves) the staging stores in C cost what the
     // spread saved (64-patch shard 4.16 vs 4.10 M), profiles/r05_ab/dist_max_upd_ab.txt
-#ifndef FPM_SPREAD4
-#define FPM_SPREAD4 0  // A/B knob: the spread object update at KS 4 too
-#endif
-    constexpr bool kSpreadUpd = KS == 8 || (FPM_SPREAD4 && KS == 4);
+    // (round 6, with the arithmetic slot_kx: at KS 4 still 0.5 % slower,
+    // profiles/r06_ab/dist_tail_pairs_spread4_ab.txt)
+    constexpr bool kSpreadUpd = KS == 8;
     static_assert(!kSpreadUpd || 3 * NOWN * 96 <= (NG - NOWN) * XTILE, "staging fits the idle groups' tiles");
     float2 *upd_f = scr_all + NOWN * XTILE, *upd_o = upd_f + NOWN * 96, *upd_p = upd_o + NOWN * 96;
     constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
@@ -483,9 +482,16 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // KS 4 / 8, so the sums overlap the row DFTs instead of following them
         // on the same groups (round 3: C 7.5k cycles per LED on the parts
         // that own a tail row vs 3.2k on the part that owns none, at KS 4)
-        // the sum of tail pixel pp over its row's 16 values per lane, e[]
-        auto tail_sum = [&](int pp, const float2 (&e)[16]) {
+        for (int pp = NG - 1 - g; pp < a.n_tail_px; pp += NG) {
+            if ((tpq[pp] % KS) != hown) continue;  // group-uniform
             const int2 px = tpx[pp];
+            const int row = NROWS + tpq[pp];
+            // the row's 16 values first: one L2 round trip (loads interleaved
+            // with the twiddle recurrence waited for each in turn, 16 round
+            // trips on every part that owns a tail row)
+            float2 e[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) e[m] = cld(ra, row * NP + t + 16 * m);
             pf2 s2p = {0.f, 0.f};
             pf2 wk = pin(tw[(t * (px.y + NP)) & (NP - 1)]);
             const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
@@ -498,56 +504,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
             s2.x = row16_sum(s2.x);  // the group's 16 lanes (DPP, bit-identical to the xor butterfly)
             s2.y = row16_sum(s2.y);
             if (t == 0) tailF[pp] = s2;
-        };
-        // the row's 16 values first: one L2 round trip (loads interleaved
-        // with the twiddle recurrence waited for each in turn, 16 round
-        // trips on every part that owns a tail row)
-        auto tail_row = [&](int pp, float2 (&e)[16]) {
-            const int row = NROWS + tpq[pp];
-#pragma unroll
-            for (int m = 0; m < 16; ++m) e[m] = cld(ra, row * NP + t + 16 * m);
-        };
-        if constexpr (KS == 8) {
-            // KS 8 (round 6): the part that owns the long tail row (17 of the
-            // 19 pixels at r 33) ran pass C 0.6-0.8k cycles longer than the
-            // others, which waited for it at sync 3 (per-part stamps).  Here a
-            // group sums two consecutive pixels -- the same row as a rule, so
-            // its 16 loads serve both -- on the 16 groups of waves 2, 3, 6 and
-            // 7, the SIMDs without a row-DFT wave
-            const int tslot = (w == 2 || w == 3) ? 4 * (w - 2) + gg : (w >= 6) ? 8 + 4 * (w - 6) + gg : -1;
-            for (int p0 = 2 * tslot; tslot >= 0 && p0 < a.n_tail_px; p0 += 32) {  // group-uniform
-                const bool own0 = (tpq[p0] % KS) == hown;
-                const bool own1 = p0 + 1 < a.n_tail_px && (tpq[p0 + 1] % KS) == hown;
-                if (!own0 && !own1) continue;
-                float2 e[16];
-                tail_row(own0 ? p0 : p0 + 1, e);
-                if (own0) tail_sum(p0, e);
-                if (own1) {
-                    if (own0 && tpq[p0 + 1] != tpq[p0]) tail_row(p0 + 1, e);  // another row (rare)
-                    tail_sum(p0 + 1, e);
-                }
-            }
-        } else {
-            for (int pp = NG - 1 - g; pp < a.n_tail_px; pp += NG) {
-                if ((tpq[pp] % KS) != hown) continue;  // group-uniform
-                const int2 px = tpx[pp];
-                const int row = NROWS + tpq[pp];
-                float2 e[16];
-#pragma unroll
-                for (int m = 0; m < 16; ++m) e[m] = cld(ra, row * NP + t + 16 * m);
-                pf2 s2p = {0.f, 0.f};
-                pf2 wk = pin(tw[(t * (px.y + NP)) & (NP - 1)]);
-                const pf2 wstep = pin(tw[(16 * (px.y + NP)) & (NP - 1)]);
-#pragma unroll
-                for (int m = 0; m < 16; ++m) {
-                    s2p += pmul(pin(e[m]), wk);
-                    if (m < 15) wk = pmul(wk, wstep);
-                }
-                float2 s2 = pout(s2p);
-                s2.x = row16_sum(s2.x);  // the group's 16 lanes (DPP, bit-identical to the xor butterfly)
-                s2.y = row16_sum(s2.y);
-                if (t == 0) tailF[pp] = s2;
-            }
         }
         __syncthreads();  // tailF
         FPM_STAMP(5)
