@@ -108,21 +108,6 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
     // (round 6, with the arithmetic slot_kx: at KS 4 still 0.5 % slower,
     // profiles/r06_ab/dist_tail_pairs_spread4_ab.txt)
     constexpr bool kSpreadUpd = KS == 8;
-#ifndef FPM_TAILFFT
-#define FPM_TAILFFT 1
-#endif
-    // Tail rows as full 256-point row transforms (round 6, KS 4 / 8): the
-    // part owning the long tail row (17 of the 19 tail pixels at r 33) ran
-    // its direct sums -- 256 columns x 17 terms in pass A, 17 pixel sums in
-    // pass C -- 0.6-0.8k cycles longer than the others, which waited for it
-    // at sync 3 (per-part stamps).  A tail row is now one more row IDFT (A)
-    // and row DFT (C) through the same code as the FFT rows, on a spare group
-    // -- the last groups, NG - 1 - j for the part's j-th tail row, clear of
-    // the spread update's staging tiles -- with its pixels moved in and out
-    // of the slot layout: every part runs one row transform's latency.
-    constexpr int kTailPerPart = (MAXTAILROWS + KS - 1) / KS;
-    constexpr bool kTailFFT = FPM_TAILFFT && KS >= 4;
-    static_assert(!kTailFFT || (NG - kTailPerPart >= NOWN + (kSpreadUpd ? 8 : 0)), "spare groups clear of rows and staging");
     static_assert(!kSpreadUpd || 3 * NOWN * 96 <= (NG - NOWN) * XTILE, "staging fits the idle groups' tiles");
     float2 *upd_f = scr_all + NOWN * XTILE, *upd_o = upd_f + NOWN * 96, *upd_p = upd_o + NOWN * 96;
     constexpr int TILES_OFF = kTgRows * NP, PMX_OFF = TILES_OFF + KS * kWinTiles;
@@ -307,36 +292,21 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         if (tid == 0) omx[0] = omx[1] = 0u;  // read by the previous LED's merge, two barriers ago
         __syncthreads();  // tailX
         FPM_STAMP(0)
-        // this group's tail row (kTailFFT): the part's j-th, on group NG - 1 - j
-        const int tj = NG - 1 - g, tq = hown + KS * tj;
-        const bool tgrp = kTailFFT && tj < kTailPerPart && tq < a.n_tail_rows;  // group-uniform
-        if (g < NOWN || tgrp) {  // group-uniform
+        if (g < NOWN) {  // group-uniform
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = make_float2(0.f, 0.f);
-            if (g < NOWN) {
 #pragma unroll
-                for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
-            } else {
-                const int p0 = a.tail_row_p0[tq], np_ = a.tail_row_np[tq], kx0 = a.tail_row_kx0[tq];
-#pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    const int p = slot_kx(t, s) - kx0;
-                    const bool in = p >= 0 && p < np_;
-                    const float2 x = tailX[p0 + (in ? p : 0)];
-                    v[SK[s]] = in ? x : make_float2(0.f, 0.f);
-                }
-            }
+            for (int s = 0; s < 6; ++s) v[SK[s]] = pout(pmul(pin(Opre[s]), pin(P[s])));   // :364
             idft256_in6(v, r, scr, wt, t, xrd);
-            if (g >= NOWN || ron) {
-                const int trow = g < NOWN ? irow : NROWS + tq;
+            if (ron) {
 #pragma unroll
-                for (int m = 0; m < 16; ++m) cst(ra, trow * NP + t + 16 * m, r[m]);
+                for (int m = 0; m < 16; ++m) cst(ra, irow * NP + t + 16 * m, r[m]);
             }
         }
         // own tail rows: direct sums over the row's pixels for every column x,
         // on the LAST waves (the FFT-row groups g < NOWN sit in the first
         // waves, so at KS 4 / 8 the sums run beside the row IDFTs)
-        for (int q = hown; !kTailFFT && q < a.n_tail_rows; q += KS) {
+        for (int q = hown; q < a.n_tail_rows; q += KS) {
             const int p0 = a.tail_row_p0[q], np_ = a.tail_row_np[q];
             for (int x = NT - 1 - tid; x < NP; x += NT) {
                 const int ti = (x * (a.tail_row_kx0[q] + NP)) & (NP - 1);
@@ -485,25 +455,14 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
 
         // ---- C: row DFTs of the own rows (full input) -> F (:394)
         float2 F[6];
-        if (g < NOWN || tgrp) {
-            const int trow = g < NOWN ? irow : NROWS + tq;
-            const bool tin = g < NOWN ? ron : true;
+        if (g < NOWN) {
 #pragma unroll
-            for (int m = 0; m < 16; ++m) v[m] = tin ? cld(ra, trow * NP + t + 16 * m) : make_float2(0.f, 0.f);
+            for (int m = 0; m < 16; ++m) v[m] = ron ? cld(ra, irow * NP + t + 16 * m) : make_float2(0.f, 0.f);
             dft256_out6(v, F, scr, wt, t, xrd);
-            if (kTailFFT && g >= NOWN) {  // the tail row's pixels out of the slot layout
-                const int p0 = a.tail_row_p0[tq], np_ = a.tail_row_np[tq], kx0 = a.tail_row_kx0[tq];
-#pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    const int p = slot_kx(t, s) - kx0;
-                    if (p >= 0 && p < np_) tailF[p0 + p] = F[s];
-                    F[s] = make_float2(0.f, 0.f);
-                }
-            }
 #ifdef FPM_DIST_SUBSTAMP
             FPM_STAMP(11)  // C: own FFT rows (waves with rows)
 #endif
-            if (kSpreadUpd && g < NOWN) {
+            if constexpr (kSpreadUpd) {
                 // stage F, O, P of the row's slots for the spread update below
                 // in the idle groups' exchange tiles (no transform uses them in C)
 #pragma unroll
@@ -523,7 +482,7 @@ __global__ void __launch_bounds__(512, 1) k_fused_dist(FusedArgs a) {
         // KS 4 / 8, so the sums overlap the row DFTs instead of following them
         // on the same groups (round 3: C 7.5k cycles per LED on the parts
         // that own a tail row vs 3.2k on the part that owns none, at KS 4)
-        for (int pp = NG - 1 - g; !kTailFFT && pp < a.n_tail_px; pp += NG) {
+        for (int pp = NG - 1 - g; pp < a.n_tail_px; pp += NG) {
             if ((tpq[pp] % KS) != hown) continue;  // group-uniform
             const int2 px = tpx[pp];
             const int row = NROWS + tpq[pp];
