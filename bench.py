@@ -64,7 +64,8 @@ WORKLOADS = {
     "c2": "config 2: dataset_mono.json with the dome fallback (Np=90, L=360, naRadius 30, 193 LEDs), "
           "64 patches, one runFPM iteration per step",
     "c2np256": "config 2 geometry at Np=256: dataset_mono.json with the dome fallback, cropSizeX 256 (L=1024, "
-               "naRadius 84, 193 LEDs; general path), 64 patches, one runFPM iteration per step",
+               "naRadius 84, 193 LEDs; general path on the Np 256 register kernels), 64 patches, one runFPM "
+               "iteration per step",
 }
 
 
@@ -152,8 +153,9 @@ def load_pmc(path, kernel):
     pl = d.get("per_launch_hbm_bytes", {})
     if kernel == "general_led_step":
         # one LED step of the general path = its per-LED launches (the Np 1024
-        # register kernels or the LDS kernels, then the tile maxima)
-        ks = [k for k in ("k_rows1024_inv", "k_cols1024", "k_rows1024_fwd", "k_gather_rowifft_tiled",
+        # / Np 256 register kernels or the LDS kernels, then the tile maxima)
+        ks = [k for k in ("k_rows1024_inv", "k_cols1024", "k_rows1024_fwd", "k_rows256_inv", "k_cols256",
+                          "k_rows256_fwd", "k_gather_rowifft_tiled",
                           "k_colpass_wave", "k_colpass_tiled", "k_rowfft_update_tiled", "k_tile_rows",
                           "k_pupil_commit") if k in pl]
         return (sum(pl[k] for k in ks) if ks else None, {k: d.get("derived", {}).get(k) for k in ks},

@@ -51,8 +51,11 @@ bool fused_small_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                         const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                         const FftPlan &pl, unsigned long long *dbg, hipStream_t s);
-// Np 1024 register row/column kernels of the general path (np1024.hip)
+// Np 1024 / Np 256 register row/column kernels of the general path
+// (np1024.hip, np256.hip; both fold the pupil commit into the next LED)
 bool np1024_supported(int np, int r);
+bool np256_supported(int np, int r, int L, bool fp16);
+bool commit_folded(const DevState &st);
 hipError_t launch_fused_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                   const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                   int ks, unsigned long long *dbg, float2 *xch, int *flags, int stall_led,
@@ -428,9 +431,14 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &st.tmax, (size_t)B * st.ntx * st.nty))) return fail(rc);
     if ((rc = dalloc(c, &st.tdirty, (size_t)B * ((st.ntx * st.nty + 31) / 32)))) return fail(rc);
     // Np 1024 general path: register row/column kernels reading the stack
-    // transposed; their row IDFT writes one max|P| partial per box row
+    // transposed; Np 256 beyond the fused kernels' radius: register kernels
+    // reading the fused column layout (g = 16).  Their row IDFT writes one
+    // max|P| partial per box row
     const bool reg1024 = c->path == FPM_PATH_GENERAL && np1024_supported(np, r) && !getenv("FPM_NO_REG1024");
-    st.npart = (c->path == FPM_PATH_GENERAL) ? (reg1024 ? std::max(pupil_parts(nb), nb) : pupil_parts(nb)) : 1;
+    const bool reg256 =
+        c->path == FPM_PATH_GENERAL && np256_supported(np, r, L, fp16) && !getenv("FPM_NO_REG256");
+    st.npart = (c->path == FPM_PATH_GENERAL) ? (reg1024 || reg256 ? std::max(pupil_parts(nb), nb) : pupil_parts(nb))
+                                             : 1;
     if ((rc = dalloc(c, &st.pmax, (size_t)B * st.npart))) return fail(rc);
     if ((rc = dalloc(c, &c->disk_dev, disk.size()))) return fail(rc);
     if ((rc = dalloc(c, &c->meas, (size_t)prob->n_stack * B * np * np))) return fail(rc);
@@ -439,6 +447,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     if ((rc = dalloc(c, &c->y0_dev, (size_t)prob->n_stack))) return fail(rc);
     if (c->path == FPM_PATH_GENERAL) {
         if (reg1024) c->meas_g = np;
+        if (reg256) c->meas_g = 16;
         // fp16 spectrum storage on the Np 1024 register kernels: the row /
         // column scratch T block-scaled in fp16 too (half its HBM traffic;
         // FPM_T32=1 keeps it fp32)
@@ -655,9 +664,9 @@ hipError_t launch_group_chain(const fpm_ctx *c, const DevState &v, hipStream_t s
         const int led = c->order[i];
         HIP_RET(launch_general_step(v, led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0, s));
     }
-    // Np 1024: the last LED's pupil commit (the others are folded into the
-    // next LED's row IDFT)
-    if (c->meas_g == c->st.np && c->st.np == 1024) HIP_RET(launch_pupil_commit(v, s));
+    // Np 1024 / 256 register kernels: the last LED's pupil commit (the others
+    // are folded into the next LED's row IDFT)
+    if (commit_folded(v)) HIP_RET(launch_pupil_commit(v, s));
     return hipSuccess;
 }
 
@@ -692,7 +701,7 @@ hipError_t launch_general_iteration(fpm_ctx *c, hipStream_t s) {
             HIP_RET(launch_general_step(view[g], led, c->x0[led], c->y0[led], c->pl_np, c->tw_np, i == 0,
                                         group_stream(c, g, s)));
     }
-    if (c->meas_g == c->st.np && c->st.np == 1024)
+    if (commit_folded(c->st))
         for (int g = 0; g < G; ++g) HIP_RET(launch_pupil_commit(view[g], group_stream(c, g, s)));
     return join_groups(c, s);
 }

@@ -838,6 +838,14 @@ static bool fft_fits(const FftPlan &pl, int lc, int nt = kFftThreads, int e = kF
 
 hipError_t launch_np1024_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, bool commit,
                                    hipStream_t s);
+hipError_t launch_np256_rows_cols(const DevState &st, const StepArgs &sa, const float2 *tw, bool commit,
+                                  hipStream_t s);
+
+// the register row / column kernels (np1024.hip, np256.hip) fold the pupil
+// commit into the next LED's row IDFT
+bool commit_folded(const DevState &st) {
+    return (st.np == 1024 && st.meas_g == 1024) || (st.np == 256 && st.meas_g == 16);
+}
 
 // first: the iteration's first LED (Np 1024: no pupil commit pending)
 hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, const FftPlan &pl,
@@ -849,6 +857,10 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
     if (st.np == 1024 && st.meas_g == 1024) {
         // Np 1024: register-resident row/column transforms (np1024.hip)
         const hipError_t e = launch_np1024_rows_cols(st, sa, tw, !first, s);
+        if (e != hipSuccess) return e;
+    } else if (st.np == 256 && st.meas_g == 16) {
+        // Np 256 beyond the fused kernels' radius: register row/column transforms (np256.hip)
+        const hipError_t e = launch_np256_rows_cols(st, sa, tw, !first, s);
         if (e != hipSuccess) return e;
     } else {
         const size_t lds = 2 * (size_t)st.np * sizeof(float2);
@@ -919,9 +931,10 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<1024>), dim3(nrow, st.B), dim3(1024), 0, s, st, sa);
     else
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tile_rows<256>), dim3(nrow, st.B), dim3(256), 0, s, st, sa);
-    // Np 1024: the commit is folded into the next LED's row IDFT (np1024.hip)
-    // and runs here only after the iteration's last LED (launch_pupil_commit)
-    if (!(st.np == 1024 && st.meas_g == 1024))
+    // Np 1024 / 256 register kernels: the commit is folded into the next LED's
+    // row IDFT and runs here only after the iteration's last LED
+    // (launch_pupil_commit)
+    if (!commit_folded(st))
         hipLaunchKernelGGL(k_pupil_commit, dim3(st.npart, st.B), dim3(kCommitThreads), 0, s, st);
     return hipGetLastError();
 }

@@ -57,7 +57,8 @@ def short(name):
     for k in ("k_fused_mr", "k_fused_small", "k_fused_s90", "k_meas_layout", "k_meas_transpose_tiles", "k_meas_transpose",
               "k_fft_batch<true>", "k_fft_batch<false>", "k_crop_rows600", "k_crop_cols600", "k_crop_rows",
               "k_crop_cols", "k_colpass_wave", "k_colpass_tiled", "k_gather_rowifft_tiled",
-              "k_rowfft_update_tiled", "k_rows1024_inv", "k_rows1024_fwd", "k_cols1024", "k_tile_rows",
+              "k_rowfft_update_tiled", "k_rows1024_inv", "k_rows1024_fwd", "k_cols1024", "k_rows256_inv",
+              "k_rows256_fwd", "k_cols256", "k_tile_rows",
               "k_tile_max_all", "k_row_max_all", "k_pupil_commit"):
         if k in name:
             return k
