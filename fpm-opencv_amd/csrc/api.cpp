@@ -463,9 +463,12 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         // patch groups on concurrent streams (FPM_PATCH_GROUPS=n overrides):
         // two for the Np 1024 kernels, whose row launches cover a few patches
         // in 1.3 rounds of workgroups (config 5, 8 patches: 65.5 -> 57.5 ms of
-        // LED steps per iteration; 3 or 4 groups measured slower, 79 / 77 ms)
+        // LED steps per iteration; 3 or 4 groups measured slower, 79 / 77 ms),
+        // and for the Np 256 register kernels, whose three short launches per
+        // LED then overlap one group's tail with the other's start (dataset_mono
+        // at Np 256, 64 patches: 1.18 -> 1.25 M LED-updates/s)
         const char *pg = getenv("FPM_PATCH_GROUPS");
-        c->ngroups = pg ? atoi(pg) : (reg1024 ? 2 : 1);
+        c->ngroups = pg ? atoi(pg) : (reg1024 || reg256 ? 2 : 1);
         c->ngroups = std::max(1, std::min({c->ngroups, B, (int)fpm_ctx::kMaxGroups}));
         for (int g = 1; g < c->ngroups; ++g) {
             if (hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking) != hipSuccess ||

@@ -859,9 +859,9 @@ hipError_t launch_general_step(const DevState &st, int led, int x0, int y0, cons
         const hipError_t e = launch_np1024_rows_cols(st, sa, tw, !first, s);
         if (e != hipSuccess) return e;
     } else if (st.np == 256 && st.meas_g == 16) {
-        // Np 256 beyond the fused kernels' radius: register row/column transforms (np256.hip)
-        const hipError_t e = launch_np256_rows_cols(st, sa, tw, !first, s);
-        if (e != hipSuccess) return e;
+        // Np 256 beyond the fused kernels' radius: register row/column
+        // transforms (np256.hip); K4 runs inside its R2, K5 folded into the next R1
+        return launch_np256_rows_cols(st, sa, tw, !first, s);
     } else {
         const size_t lds = 2 * (size_t)st.np * sizeof(float2);
         // row kernels: up to 16 box rows per block, fewer while a few large

@@ -16,10 +16,14 @@
 //                      column layout (meas_layout g = 16: lane t holds rows
 //                      t + 16 m of its column, 32 contiguous bytes), column
 //                      DFT, box rows back to T
-//   R2 k_rows256_fwd   a group per box row: T row in, row DFT, object update
-//                      and pupil numerator on the row's disk pixels
-// general.hip's K4 (tile maxima) follows each LED; K5 (the commit) runs only
-// after an iteration's last LED (launch_pupil_commit).
+//   R2 k_rows256_fwd   a block per 16-row tile row of the spectrum, a group
+//                      per box row: T row in, row DFT, object update and pupil
+//                      numerator on the row's disk pixels, then the tile
+//                      maxima of the window's tiles in that tile row and the
+//                      tile row's maximum (general.hip K4's values, bit for
+//                      bit: 1.01 -> 1.18 M LED-updates/s at dataset_mono Np 256)
+// Three launches per LED: K4 is inside R2, and K5 (the commit) runs only after
+// an iteration's last LED (launch_pupil_commit).
 //
 // Natural layout everywhere: lane t of a group holds elements t + 16 j (j =
 // 0..15) of its row / column, which is both dft256_full's input and output
@@ -27,8 +31,8 @@
 //
 // Blocks are mapped so that every kernel's blocks of patch b land on XCD
 // b mod 8 (round-robin dispatch; only a placement, correctness does not
-// depend on it): a patch's T (nb x 256 x 8 B = 346 KB at r 84) is written and
-// read back on one XCD.
+// depend on it): a patch's T (nb x 256 x 8 B = 346 KB at r 84), window and
+// pupil are written and read back on one XCD.
 #include <hip/hip_runtime.h>
 
 #include "cpk.hpp"
@@ -63,21 +67,21 @@ __device__ __forceinline__ float row16_max_nonneg(float x) {
     return __uint_as_float(v);
 }
 
-// block -> (patch b, sub-block) of a 1-D grid of nsub * B blocks, patch b on
-// XCD b mod 8 when B is a multiple of 8
-__device__ __forceinline__ void xcd_block(int nsub, int B, int &b, int &sub) {
+// block -> (patch b, sub-block) of a 1-D grid of nsub * xcd_patches(B)
+// blocks, patch b on XCD b mod 8; false for the padding blocks of patches
+// b >= B (B not a multiple of 8), which exit at once.  Against the plain
+// b = block / nsub: 1.20-1.22 -> 1.22-1.24 M at dataset_mono Np 256, 64
+// patches (profiles/r06_ab/np256_register_path_ab.txt)
+__host__ __device__ __forceinline__ int xcd_patches(int B) { return (B + 7) & ~7; }
+__device__ __forceinline__ bool xcd_block(int nsub, int B, int &b, int &sub) {
     const int id = blockIdx.x;
-    if ((B & 7) == 0) {
-        const int k = id >> 3, q = k / nsub;
-        b = (id & 7) + 8 * q;
-        sub = k - q * nsub;
-    } else {
-        b = id / nsub;
-        sub = id - b * nsub;
-    }
+    const int k = id >> 3, q = k / nsub;
+    b = (id & 7) + 8 * q;
+    sub = k - q * nsub;
+    return b < B;
 }
 
-// R1: grid (ceil(nb / GPB) * B), block NT, LDS (N + GPB XTILE_H) complex
+// R1: grid (ceil(nb / GPB) * xcd_patches(B)), block NT, LDS (N + GPB XTILE_H) complex
 __global__ void __launch_bounds__(n256::NT) k_rows256_inv(DevState st, StepArgs sa, const float2 *__restrict__ tw,
                                                           int commit) {
     using namespace n256;
@@ -86,7 +90,7 @@ __global__ void __launch_bounds__(n256::NT) k_rows256_inv(DevState st, StepArgs 
     const int g = threadIdx.x >> 4, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const int r = st.r, nb = st.nb;
     int b, sub;
-    xcd_block((nb + GPB - 1) / GPB, st.B, b, sub);
+    if (!xcd_block((nb + GPB - 1) / GPB, st.B, b, sub)) return;  // block-uniform
     const int row = sub * GPB + g;
     // the twiddle, the previous LED's tile-row maxima and the first half
     // row's loads all issued before the first store or barrier (np1024.hip R1)
@@ -163,14 +167,14 @@ __global__ void __launch_bounds__(n256::NT) k_rows256_inv(DevState st, StepArgs 
     for (int k = 0; k < 16; ++k) T[16 * k] = y[k];
 }
 
-// C: grid ((N / GPB) * B), block NT, LDS (N + max(nb SP, GPB XTILE_H)) complex
+// C: grid ((N / GPB) * xcd_patches(B)), block NT, LDS (N + max(nb SP, GPB XTILE_H)) complex
 __global__ void __launch_bounds__(n256::NT) k_cols256(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n256;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int g = threadIdx.x >> 4, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
     const int r = st.r, nb = st.nb;
     int b, sub;
-    xcd_block(N / GPB, st.B, b, sub);
+    if (!xcd_block(N / GPB, st.B, b, sub)) return;  // block-uniform
     const int x0 = sub * GPB;
     const float2 twv = tw[threadIdx.x];
     float2 *twL = sm;
@@ -234,22 +238,42 @@ __global__ void __launch_bounds__(n256::NT) k_cols256(DevState st, StepArgs sa, 
     for (int idx = threadIdx.x; idx < tot; idx += NT) T[(size_t)(idx / GPB) * N + (idx % GPB)] = strip[(idx / GPB) * SP + (idx % GPB)];
 }
 
-// R2: grid (ceil(nb / GPB) * B), block NT, LDS as R1
+// R2: grid (ntr * xcd_patches(B)), block NT, LDS as R1: one block per 16-row tile row of
+// the spectrum (ntr = the most tile rows a window of nb rows spans), group g
+// on spectrum row 16 ty + g.  After the update the block re-reads its tile
+// row's window tiles and writes their maxima and the tile row's maximum --
+// general.hip K4's values, bit for bit, without its launch.
+constexpr int kMaxWinTiles = (2 * (n256::H - 1) + 15) / kTile + 1;  // tile columns a window spans, r < 128
 __global__ void __launch_bounds__(n256::NT) k_rows256_fwd(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n256;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     __shared__ float red[WPB];
+    __shared__ float tred[WPB][kMaxWinTiles];
     const int g = threadIdx.x >> 4, t = threadIdx.x & 15, xrd = exch_rbase_half(t);
-    const int r = st.r, nb = st.nb;
+    const int r = st.r, nb = st.nb, L = st.L;
+    const int ty0 = (sa.yc - r) / kTile, ty1 = (sa.yc + r) / kTile;
     int b, sub;
-    xcd_block((nb + GPB - 1) / GPB, st.B, b, sub);
-    const int row = sub * GPB + g;
+    if (!xcd_block((2 * r + 15) / kTile + 1, st.B, b, sub)) return;  // block-uniform
+    const int ty = ty0 + sub;
+    if (ty > ty1) return;  // block-uniform, before any barrier
+    const int row = ty * kTile + g - (sa.yc - r);  // box row of this group's spectrum row
+    const bool act = row >= 0 && row < nb;
+    // the tile row's maxima outside the window: unchanged by this launch,
+    // their loads issued first
+    const int tx0 = (sa.xc - r) / kTile, tx1 = (sa.xc + r) / kTile, ntx = st.ntx;
+    float *tmax = st.tmax + ((size_t)b * st.nty + ty) * ntx;
+    float tm[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = threadIdx.x + NT * k;
+        tm[k] = tmax[i < ntx ? i : 0];
+    }
     const float2 twv = tw[threadIdx.x];
     float2 *twL = sm;
     float2 *wt = sm + N + g * XTILE_H;
     // the row's T first (its latency runs under the max|P| reduction), then
     // max|P| of the previous commit from the npart <= NT partial maxima (:415)
-    const int rowc = row < nb ? row : nb - 1;
+    const int rowc = act ? row : (row < 0 ? 0 : nb - 1);
     const float2 *Tr = st.T + ((size_t)b * nb + rowc) * N + t;
     float2 x[16];
 #pragma unroll
@@ -258,39 +282,80 @@ __global__ void __launch_bounds__(n256::NT) k_rows256_fwd(DevState st, StepArgs 
     const float pv = st.pmax[(size_t)b * st.npart + (i < st.npart ? i : 0)];
     sm[threadIdx.x] = twv;
     const float pm = block_max_nonneg(i < st.npart ? pv : 0.f, red);  // its barriers publish the twiddles
-    if (row >= nb) return;  // group-uniform
-    const int ky = row - r, w2 = r * r - ky * ky;
-    float2 F[16];
-    dft256_full<false, true>(x, F, wt, LdsTw{twL, t, 1}, t, xrd);  // :394 (rows); F[k] = X[t + 16 k]
-    float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
-    float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
-    float2 *sp = st.spec + (size_t)b * st.L * st.L + (size_t)(sa.yc + ky) * st.L + sa.xc;
-    // half the row's loads ahead of their stores (the stores may alias the
-    // loads, so the compiler keeps program order otherwise)
+    float2 *sp0 = st.spec + (size_t)b * L * L;
+    if (act) {  // group-uniform
+        const int ky = row - r, w2 = r * r - ky * ky;
+        float2 F[16];
+        dft256_full<false, true>(x, F, wt, LdsTw{twL, t, 1}, t, xrd);  // :394 (rows); F[k] = X[t + 16 k]
+        float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
+        float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
+        float2 *sp = sp0 + (size_t)(sa.yc + ky) * L + sa.xc;
+        // half the row's loads ahead of their stores (the stores may alias the
+        // loads, so the compiler keeps program order otherwise)
 #pragma unroll
-    for (int hp = 0; hp < 2; ++hp) {
-        float2 ov[8], pp[8];
+        for (int hp = 0; hp < 2; ++hp) {
+            float2 ov[8], pp[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int kx = fold256(t + 16 * (8 * hp + k));
-            const int kc = kx * kx <= w2 ? kx : 0;
-            pp[k] = pup[kc];
-            ov[k] = sp[kc];
-        }
+            for (int k = 0; k < 8; ++k) {
+                const int kx = fold256(t + 16 * (8 * hp + k));
+                const int kc = kx * kx <= w2 ? kx : 0;
+                pp[k] = pup[kc];
+                ov[k] = sp[kc];
+            }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int kx = fold256(t + 16 * (8 * hp + k));
-            if (kx * kx > w2) continue;
-            const float2 o = ov[k];                                 // pre-update Objfcrop (:361)
-            const float2 p = pp[k];
-            const float2 D = csub(F[8 * hp + k], cmul(o, p));       // Objfup - ObjfcropP (:409,463)
-            const float pa = cmag(p);                               // object update (:406-419,433)
-            const float2 dpc = cmul(cmul(D, cscale(cconj(p), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
-            sp[kx] = cadd(o, dpc);
-            const float oa = cmag(o);                               // pupil numerator (:459-464,469)
-            dP[kx] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
+            for (int k = 0; k < 8; ++k) {
+                const int kx = fold256(t + 16 * (8 * hp + k));
+                if (kx * kx > w2) continue;
+                const float2 o = ov[k];                                 // pre-update Objfcrop (:361)
+                const float2 p = pp[k];
+                const float2 D = csub(F[8 * hp + k], cmul(o, p));       // Objfup - ObjfcropP (:409,463)
+                const float pa = cmag(p);                               // object update (:406-419,433)
+                const float2 dpc = cmul(cmul(D, cscale(cconj(p), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
+                sp[kx] = cadd(o, dpc);
+                const float oa = cmag(o);                               // pupil numerator (:459-464,469)
+                dP[kx] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
+            }
         }
     }
+    // max|objF| bookkeeping (:460,467): the window's tiles of this tile row
+    // re-read after the block's stores (workgroup scope: one L1 per block),
+    // group g reading row g of every tile, every load issued before the first
+    // reduction (clamped in-bounds, masked)
+    __syncthreads();
+    const int yy = ty * kTile + g;
+    float m[kMaxWinTiles];
+#pragma unroll
+    for (int k = 0; k < kMaxWinTiles; ++k) {
+        const int xx = (tx0 + k) * kTile + t;
+        const bool ok = tx0 + k <= tx1 && yy < L && xx < L;
+        const float2 v = sp0[ok ? (size_t)yy * L + xx : 0];
+        m[k] = ok ? cmag(v) : 0.f;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kMaxWinTiles; ++k) {
+        if (tx0 + k <= tx1) {  // block-uniform
+            const float v = wave_max_nonneg(m[k]);
+            if (lane == 0) tred[w][k] = v;
+        }
+    }
+    __syncthreads();
+    float mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int ix = threadIdx.x + NT * k;
+        if (ix >= ntx) continue;
+        float v = tm[k];
+        if (ix >= tx0 && ix <= tx1) {
+            v = tred[0][ix - tx0];
+#pragma unroll
+            for (int ww = 1; ww < WPB; ++ww) v = fmaxf(v, tred[ww][ix - tx0]);
+            tmax[ix] = v;
+        }
+        mx = fmaxf(mx, v);
+    }
+    mx = block_max_nonneg(mx, red);
+    if (threadIdx.x == 0) st.rmax[(size_t)b * st.nty + ty] = mx;
 }
 
 }  // namespace
@@ -310,10 +375,11 @@ hipError_t launch_np256_rows_cols(const DevState &st, const StepArgs &sa, const 
         return hipErrorInvalidValue;
     const size_t lds_r = (size_t)(N + GPB * XTILE_H) * sizeof(float2);
     const size_t lds_c = (size_t)(N + std::max(st.nb * SP, GPB * XTILE_H)) * sizeof(float2);
-    const int nsr = (st.nb + GPB - 1) / GPB;
-    hipLaunchKernelGGL(k_rows256_inv, dim3(nsr * st.B), dim3(NT), lds_r, s, st, sa, tw, commit ? 1 : 0);
-    hipLaunchKernelGGL(k_cols256, dim3((N / GPB) * st.B), dim3(NT), lds_c, s, st, sa, tw);
-    hipLaunchKernelGGL(k_rows256_fwd, dim3(nsr * st.B), dim3(NT), lds_r, s, st, sa, tw);
+    const int nsr = (st.nb + GPB - 1) / GPB, Bp = xcd_patches(st.B);
+    hipLaunchKernelGGL(k_rows256_inv, dim3(nsr * Bp), dim3(NT), lds_r, s, st, sa, tw, commit ? 1 : 0);
+    hipLaunchKernelGGL(k_cols256, dim3((N / GPB) * Bp), dim3(NT), lds_c, s, st, sa, tw);
+    const int ntr = (2 * st.r + 15) / kTile + 1;  // tile rows a window can span
+    hipLaunchKernelGGL(k_rows256_fwd, dim3(ntr * Bp), dim3(NT), lds_r, s, st, sa, tw);
     return hipGetLastError();
 }
 
