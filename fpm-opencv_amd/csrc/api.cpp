@@ -46,11 +46,6 @@ bool fused_s90_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_s90_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
                                       const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
                                       unsigned long long *dbg, hipStream_t s);
-// Np 256 fused kernel for pupil radii beyond fpm_fused.hip's (fused_large.hip)
-bool fused_large_supported(int np, int r, const DevState &st);
-hipError_t launch_fused_large_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
-                                        const int *x0_dev, const int *y0_dev, int n_order, const float2 *tw_np,
-                                        unsigned long long *dbg, hipStream_t s);
 // small-patch fused kernel (fused_small.hip, Np <= 96)
 bool fused_small_supported(int np, int r, const DevState &st);
 hipError_t launch_fused_small_iteration(const DevState &st, const uint16_t *meas, const int *order_dev,
@@ -204,7 +199,6 @@ struct fpm_ctx {
     bool fused_mr = false;          // fused path runs the Np 200 kernel (fused_mr.hip)
     bool fused_small = false;       // fused path runs the small-patch kernel (fused_small.hip)
     bool fused_s90 = false;         // fused path runs the Np 90 kernel (fused_s90.hip)
-    bool fused_large = false;       // fused path runs the large-radius Np 256 kernel (fused_large.hip)
     int *order_dev = nullptr, *x0_dev = nullptr, *y0_dev = nullptr;
     uint8_t *disk_dev = nullptr;
     std::vector<void *> allocs;
@@ -413,11 +407,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
     // selects the generic small-patch kernel
     c->fused_s90 = !c->fused_nt && !c->fused_mr && !getenv("FPM_NO_S90") && fused_s90_supported(np, r, st);
     c->fused_small = !c->fused_nt && !c->fused_mr && !c->fused_s90 && fused_small_supported(np, r, st);
-    // Np 256 beyond the one-workgroup kernel's radius (dataset_mono at Np 256:
-    // r 84); FPM_NO_LARGE=1 leaves it to the general path's register kernels
-    c->fused_large = !c->fused_nt && !c->fused_mr && !c->fused_s90 && !c->fused_small && !fp16 &&
-                     !getenv("FPM_NO_LARGE") && fused_large_supported(np, r, st);
-    const bool fused_ok = c->fused_nt || c->fused_mr || c->fused_s90 || c->fused_small || c->fused_large;
+    const bool fused_ok = c->fused_nt || c->fused_mr || c->fused_s90 || c->fused_small;
     if (prob->path == FPM_PATH_FUSED && (fp16 || !fused_ok))
         return fail(set_err(FPM_ERR_INVAL, "fused path unsupported for Np=%d r=%d L=%d%s", np, r, L,
                             fp16 ? " with fp16 spectrum storage" : ""));
@@ -489,9 +479,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
             return fail(set_err(FPM_ERR_DEVICE, "patch-group event creation failed"));
     } else {
         c->meas_g = c->fused_small ? np : c->fused_s90 ? 9 : c->fused_mr ? 10 : 16;
-        // the large-radius kernel keeps its row scratch and numerator in global memory
-        if ((rc = dalloc(c, &st.T, c->fused_large ? (size_t)B * nb * np : fused_T_elems(np, r, B)))) return fail(rc);
-        if (c->fused_large && (rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
+        if ((rc = dalloc(c, &st.T, fused_T_elems(np, r, B)))) return fail(rc);
         int n_cu = 0;
         (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
         // small batches: every phase distributed over KS workgroups per patch
@@ -794,9 +782,6 @@ int fpm_run(fpm_ctx *c, int iters) {
         if (c->path == FPM_PATH_FUSED && c->fused_s90) {
             HIP_TRY(launch_fused_s90_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                                c->prob.n_order, c->tw_np, c->dbg, c->stream));
-        } else if (c->path == FPM_PATH_FUSED && c->fused_large) {
-            HIP_TRY(launch_fused_large_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
-                                                 c->prob.n_order, c->tw_np, c->dbg, c->stream));
         } else if (c->path == FPM_PATH_FUSED && c->fused_small) {
             HIP_TRY(launch_fused_small_iteration(c->st, c->meas, c->order_dev, c->x0_dev, c->y0_dev,
                                                  c->prob.n_order, c->tw_np, c->pl_np, c->dbg, c->stream));
@@ -989,12 +974,11 @@ static void fill_info(const fpm_ctx *c, fpm_info *info) {
     info->fused_kernel = c->path != FPM_PATH_FUSED ? FPM_KERNEL_GENERAL
                          : c->fused_s90        ? FPM_KERNEL_FUSED_NP90
                          : c->fused_small      ? FPM_KERNEL_FUSED_SMALL
-                         : c->fused_large      ? FPM_KERNEL_FUSED_NP256_LARGE
                          : c->fused_mr         ? FPM_KERNEL_FUSED_NP200
                          : c->dist             ? FPM_KERNEL_FUSED_NP256_DIST
                                                : FPM_KERNEL_FUSED_NP256;
     info->threads_per_wg = c->path != FPM_PATH_FUSED ? 0
-                           : c->fused_s90 || c->fused_small || c->fused_large ? 1024
+                           : c->fused_s90 || c->fused_small ? 1024
                            : c->fused_mr ? 768
                                          : c->fused_nt;
 }

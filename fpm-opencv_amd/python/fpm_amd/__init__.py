@@ -38,11 +38,9 @@ FLAG_SCALAR_RE_ONLY = 4     # legacy: cv::add(UMat c2, double) on the real chann
 # fpm_info.fused_kernel: the LED-update kernel of the context (fpm_hip.h FPM_KERNEL_*)
 KERNEL_GENERAL, KERNEL_FUSED_NP256, KERNEL_FUSED_NP200, KERNEL_FUSED_SMALL, KERNEL_FUSED_NP256_DIST = 0, 1, 2, 3, 4
 KERNEL_FUSED_NP90 = 5
-KERNEL_FUSED_NP256_LARGE = 6
 KERNEL_NAMES = {KERNEL_GENERAL: "general_led_step", KERNEL_FUSED_NP256: "k_fused_iteration",
                 KERNEL_FUSED_NP200: "k_fused_mr", KERNEL_FUSED_SMALL: "k_fused_small",
-                KERNEL_FUSED_NP256_DIST: "k_fused_dist", KERNEL_FUSED_NP90: "k_fused_s90",
-                KERNEL_FUSED_NP256_LARGE: "k_fused_large"}
+                KERNEL_FUSED_NP256_DIST: "k_fused_dist", KERNEL_FUSED_NP90: "k_fused_s90"}
 
 # every symbol include/fpm_hip.h declares
 HIP_SYMBOLS = (

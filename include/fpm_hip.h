@@ -131,8 +131,6 @@ typedef struct fpm_ctx fpm_ctx;
 #define FPM_KERNEL_FUSED_NP256_DIST 4  /* k_fused_dist (Np 256, every phase distributed
                                           over wg_per_patch workgroups; small batches) */
 #define FPM_KERNEL_FUSED_NP90   5  /* k_fused_s90 (Np 90: register 9 x 10 transforms) */
-#define FPM_KERNEL_FUSED_NP256_LARGE 6  /* k_fused_large (Np 256, 34 < r < 128: row scratch
-                                          in global memory, one 1024-thread workgroup per patch) */
 
 /* Which path the context runs and its per-launch geometry. */
 typedef struct fpm_info {

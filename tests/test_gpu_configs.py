@@ -101,9 +101,9 @@ def test_config2_geometry_at_np256_r84_64_patches():
     """BASELINE.md 3's "dataset_mono geometry (Np = 90 / 256)" at Np 256: the
     dome fallback at cropSizeX 256 (tests/golden/geometry_mono_dome_np256.json
     from the reference's own jsoncpp probe) gives L 1024 and naRadius 84
-    (fpmMain.cpp:305-306), beyond the one-workgroup Np 256 kernel's r <= 34,
-    so the large-radius fused kernel runs it (fused_large.hip, fpm_info); 64
-    patches, 2 iterations, sampled patches vs the C++ fp64 oracle."""
+    (fpmMain.cpp:305-306), beyond the fused Np 256 kernels' r <= 34, so the
+    general path runs it (fpm_info); 64 patches, 2 iterations, sampled patches
+    vs the C++ fp64 oracle."""
     import oracle_lib
     p, x0, y0 = _probe_geometry("geometry_mono_dome_np256.json")
     Np, L, r = p["np"], p["nlarge"], p["na_radius"]
@@ -114,7 +114,7 @@ def test_config2_geometry_at_np256_r84_64_patches():
     prob = fpm_amd.Problem(Np, L, order, x0, y0, r, p["delta1"], p["delta2"], n_patch=B)
     with fpm_amd.Solver(prob) as s:
         info = s.info()
-        assert info.path == fpm_amd.PATH_FUSED and info.fused_kernel == fpm_amd.KERNEL_FUSED_NP256_LARGE
+        assert info.path == fpm_amd.PATH_GENERAL and info.fused_kernel == fpm_amd.KERNEL_GENERAL
         assert info.box == 169
         s.upload(stack)
         s.init()

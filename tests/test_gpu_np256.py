@@ -1,10 +1,10 @@
 """Np 256 register row/column kernels of the general path (csrc/np256.hip:
 one 256-point transform per 16-lane group in registers, the stack read in the
 fused column layout g = 16) for pupil radii beyond the fused Np 256 kernels
-(r > 34; dataset_mono at cropSizeX 256 has r 84) on the general path
-(PATH_GENERAL; the automatic choice is the large-radius fused kernel,
-tests/test_gpu_fused_large.py), vs the mixed-radix LDS kernels they replace
-(FPM_NO_REG256=1 keeps the old ones) and vs the C++ fp64 oracle (GPU only).
+(r > 34; dataset_mono at cropSizeX 256 has r 84), vs the mixed-radix LDS
+kernels they replace (FPM_NO_REG256=1 keeps the old ones) and vs the C++ fp64
+oracle (GPU only).  The full-size dataset_mono case (64 patches, 193 LEDs)
+is tests/test_gpu_configs.py::test_config2_geometry_at_np256_r84_64_patches.
 
 Tolerance: relative L2 <= 1e-5 against the oracle after 1 iteration (as every
 fp32 path), <= 1e-5 between the two GPU implementations after 2 iterations.
@@ -45,7 +45,7 @@ def test_np256_register_path_equals_lds_path(L, r, B):
     else:
         x0, y0, order = grid_geometry(Np, L, 3 if L > 768 else 2, 60)
     stack = make_stack(Np, L, r, x0, y0, n_patch=B, seed=260 + r + B)
-    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=B, path=fpm_amd.PATH_GENERAL)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=B)
     with fpm_amd.Solver(prob) as s:
         assert s.info().path == fpm_amd.PATH_GENERAL
     reg = _run(prob, stack, 2, reg=True)
@@ -61,7 +61,7 @@ def test_np256_register_path_vs_oracle():
     L, r = 768, 84
     x0, y0, order = grid_geometry(Np, L, 3, 50)
     stack = make_stack(Np, L, r, x0, y0, n_patch=1, seed=265)
-    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=1, path=fpm_amd.PATH_GENERAL)
+    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=1)
     out = _run(prob, stack, 1)
     ref = oracle_lib.run_fpm(stack[:, 0], order, x0, y0, Np, L, r, 5, 10, 1)
     for k in ("objF", "objCrop", "pupil"):
@@ -75,6 +75,6 @@ def test_np256_register_path_stack_layout_round_trip():
     x0, y0, order = grid_geometry(Np, L, 2, 60)
     rng = np.random.default_rng(266)
     stack = rng.integers(0, 65535, (len(x0), 2, Np, Np)).astype(np.uint16)
-    with fpm_amd.Solver(fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2, path=fpm_amd.PATH_GENERAL)) as s:
+    with fpm_amd.Solver(fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2)) as s:
         s.upload(stack)
         np.testing.assert_array_equal(s.download_stack(), stack)

@@ -6,13 +6,12 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r06n}
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_np256.py tests/test_gpu_fused_large.py ${EXTRA_TESTS} > $O/tests.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAIL|Error|assert|rel L2" $O/tests.log | head -30; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_np256.py ${EXTRA_TESTS} > $O/tests.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAIL|Error|assert|rel L2" $O/tests.log | head -30; exit 1; }
 grep -E "passed|failed|rel L2" $O/tests.log | tail -8
 venv() {
   case $1 in
     new) echo "FPM_X=1";;
-    old) echo "FPM_NO_REG256=1 FPM_NO_LARGE=1";;
-    gen) echo "FPM_NO_LARGE=1";;
+    old) echo "FPM_NO_REG256=1";;
     g1) echo "FPM_PATCH_GROUPS=1";;
     g2) echo "FPM_PATCH_GROUPS=2";;
     g3) echo "FPM_PATCH_GROUPS=3";;
