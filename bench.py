@@ -137,7 +137,7 @@ def min_bytes_per_update(np_, support_px, meas_bytes=2):
     return float(meas_bytes) * np_ * np_ + 16.0 * support_px
 
 
-def load_pmc(path, kernel):
+def load_pmc(path, kernel, n_led=None):
     """(per-launch HBM bytes, derived counter view, note) for `kernel` from a
     tools/pmc_to_json.py file -- only when its src_hash matches the current
     csrc tree, so a profile of older kernels is never reported as traffic."""
@@ -153,13 +153,24 @@ def load_pmc(path, kernel):
     pl = d.get("per_launch_hbm_bytes", {})
     if kernel == "general_led_step":
         # one LED step of the general path = its per-LED launches (the Np 1024
-        # / Np 256 register kernels or the LDS kernels, then the tile maxima)
+        # / Np 256 register kernels or the LDS kernels, then the tile maxima).
+        # Each kernel runs once per patch group and LED (the commit of the
+        # register paths once per group and iteration): the counter file's
+        # per-dispatch bytes times its dispatches over the profiled run's LED
+        # steps (tools/gpu/prof_counters.sh: one iteration of n_led LEDs)
         ks = [k for k in ("k_rows1024_inv", "k_cols1024", "k_rows1024_fwd", "k_rows256_inv", "k_cols256",
                           "k_rows256_fwd", "k_gather_rowifft_tiled",
                           "k_colpass_wave", "k_colpass_tiled", "k_rowfft_update_tiled", "k_tile_rows",
                           "k_pupil_commit") if k in pl]
-        return (sum(pl[k] for k in ks) if ks else None, {k: d.get("derived", {}).get(k) for k in ks},
-                f"{os.path.basename(path)} (csrc {d['src_hash']}; sum of {', '.join(ks)})")
+        disp = d.get("dispatches", {})
+        if ks and n_led and all(k in disp for k in ks):
+            tot = sum(pl[k] * disp[k] for k in ks) / n_led
+            how = f"sum of per-dispatch bytes x dispatches / {n_led} LED steps of {', '.join(ks)}"
+        else:
+            tot = sum(pl[k] for k in ks) if ks else None
+            how = f"sum of per-dispatch bytes of {', '.join(ks)} (one patch group's LED step)"
+        return (tot, {k: d.get("derived", {}).get(k) for k in ks},
+                f"{os.path.basename(path)} (csrc {d['src_hash']}; {how})")
     return (pl.get(kernel), d.get("derived", {}).get(kernel),
             f"{os.path.basename(path)} (csrc {d['src_hash']})")
 
@@ -204,7 +215,7 @@ def roofline_line(geo, info, per_launch_ms, per_launch_updates, pmc_path, clock=
     np_, S = geo["np_"], info.support_px
     t = per_launch_ms * 1e-3
     kname = kernel_name(info)
-    traffic, counters, pmc_note = load_pmc(pmc_path, kname)
+    traffic, counters, pmc_note = load_pmc(pmc_path, kname, geo.get("n_led"))
     flops = algorithmic_flops_per_update(np_, info.box, S) * per_launch_updates
     achieved_tf = flops / t / 1e12
     min_bytes = min_bytes_per_update(np_, S) * per_launch_updates

@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(n256::NT) k_cols256(DevState st, StepArgs sa, 
 // row's window tiles and writes their maxima and the tile row's maximum --
 // general.hip K4's values, bit for bit, without its launch.
 constexpr int kMaxWinTiles = (2 * (n256::H - 1) + 15) / kTile + 1;  // tile columns a window spans, r < 128
-__global__ void __launch_bounds__(n256::NT) k_rows256_fwd(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
+__global__ void __launch_bounds__(n256::NT) __attribute__((amdgpu_waves_per_eu(4))) k_rows256_fwd(DevState st, StepArgs sa, const float2 *__restrict__ tw) {
     using namespace n256;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     __shared__ float red[WPB];
@@ -285,16 +285,13 @@ __global__ void __launch_bounds__(n256::NT) k_rows256_fwd(DevState st, StepArgs 
     float2 *sp0 = st.spec + (size_t)b * L * L;
     if (act) {  // group-uniform
         const int ky = row - r, w2 = r * r - ky * ky;
-        float2 F[16];
-        dft256_full<false, true>(x, F, wt, LdsTw{twL, t, 1}, t, xrd);  // :394 (rows); F[k] = X[t + 16 k]
         float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
         float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
         float2 *sp = sp0 + (size_t)(sa.yc + ky) * L + sa.xc;
         // half the row's loads ahead of their stores (the stores may alias the
         // loads, so the compiler keeps program order otherwise)
-#pragma unroll
-        for (int hp = 0; hp < 2; ++hp) {
-            float2 ov[8], pp[8];
+        float2 ov[8], pp[8];
+        auto load_half = [&](int hp) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int kx = fold256(t + 16 * (8 * hp + k));
@@ -302,6 +299,12 @@ __global__ void __launch_bounds__(n256::NT) k_rows256_fwd(DevState st, StepArgs 
                 pp[k] = pup[kc];
                 ov[k] = sp[kc];
             }
+        };
+        float2 F[16];
+        dft256_full<false, true>(x, F, wt, LdsTw{twL, t, 1}, t, xrd);  // :394 (rows); F[k] = X[t + 16 k]
+#pragma unroll
+        for (int hp = 0; hp < 2; ++hp) {
+            load_half(hp);  // (the first half issued before the transform: no change, r06_ab)
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int kx = fold256(t + 16 * (8 * hp + k));

@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIG = {"metric": "metric", "c2": "c2", "c3": "c3", "c5": "c5", "pt128": "metric", "pt64": "metric",
-          "pt32": "metric"}
+          "pt32": "metric", "c2np256": "c2", "default_cmd": None}  # None: a bench line without counters
 
 
 def led_kernel(pmc):
@@ -33,7 +33,7 @@ def main():
         pmc = os.path.join(src, f"pmc_{w}", "pmc.json")
         if os.path.exists(b):
             shutil.copy(b, os.path.join(prof, f"{rnd}_bench_{w}.json"))
-        if os.path.exists(pmc):
+        if cfg and os.path.exists(pmc):
             # the counter run of an evidence part may come without its bench
             # line (tools/gpu/r04_prof.sh runs in parts): key from the file
             kern = json.load(open(b))["config"]["kernel"] if os.path.exists(b) else led_kernel(pmc)

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 T=${TAG:-pmc}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$T
 mkdir -p $OUT
-RX="k_fused|k_meas|k_crop|k_fft|k_colpass|k_gather|k_rowfft|k_rows1024|k_cols1024|k_tile|k_pupil|k_row_max"
+RX="k_fused|k_meas|k_crop|k_fft|k_colpass|k_gather|k_rowfft|k_rows1024|k_cols1024|k_rows256|k_cols256|k_tile|k_pupil|k_row_max"
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B" \
          "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \

@@ -21,11 +21,11 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "SMOKE FAILED"; tail -5 $O/smoke.log; exit 1; }
   tail -1 $O/smoke.log
 fi
-W_ALL="metric: c2:--config_c2 c3:--config_c3 c5:--config_c5 pt128:--patches-total_128 pt64:--patches-total_64 pt32:--patches-total_32"
+W_ALL="metric: c2:--config_c2 c3:--config_c3 c5:--config_c5 pt128:--patches-total_128 pt64:--patches-total_64 pt32:--patches-total_32 c2np256:--config_c2_--np_256"
 if [ -z "$SKIP_PMC" ]; then
   for W in $W_ALL; do
     N=${W%%:*}; A=${W#*:}
-    case " ${PMC:-metric c2 c3 c5 pt128 pt64 pt32} " in *" $N "*) ;; *) continue;; esac
+    case " ${PMC:-metric c2 c3 c5 pt128 pt64 pt32 c2np256} " in *" $N "*) ;; *) continue;; esac
     TAG=$T/pmc_$N BENCH_ARGS="${A//_/ }" bash tools/gpu/prof_counters.sh || { echo "pmc $N failed"; exit 1; }
     echo "pmc $N done"
   done
@@ -43,7 +43,7 @@ bl c5 "--config c5 --steps 3 --warmup 1 --no-cpu-baseline $(pm c5)" && \
 bl pt128 "--patches-total 128 --steps 20 --warmup 3 --no-cpu-baseline $(pm pt128)" && \
 bl pt64 "--patches-total 64 --steps 20 --warmup 3 --no-cpu-baseline $(pm pt64)" && \
 bl pt32 "--patches-total 32 --steps 20 --warmup 3 --no-cpu-baseline $(pm pt32)" && \
-bl c2np256 "--config c2 --np 256 --steps 5 --warmup 1 --no-cpu-baseline" && \
+bl c2np256 "--config c2 --np 256 --steps 5 --warmup 1 --no-cpu-baseline $(pm c2np256)" && \
 bl default_cmd "" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/kt -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/kt.log 2>&1 || { echo "kernel trace rc=$?"; tail -5 $O/kt.log; exit 1; }
 find $O/kt -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_metric.csv \;

@@ -99,6 +99,7 @@ def main():
         with open(src) as fh:
             prev = json.load(fh)
         raw, stamp = prev["raw_per_launch"], prev["src_hash"]
+        disp = prev.get("dispatches", {})
     else:
         for f in sorted(glob.glob(os.path.join(src, "*", "**", "*counter_collection.csv"), recursive=True)):
             with open(f) as fh:
@@ -109,9 +110,14 @@ def main():
                     if k == "k_meas_layout" and r["Counter_Name"] == "FETCH_SIZE" and "Grid_Size" in r:
                         perm.append((int(r["Grid_Size"]), v * 1024.0))
         raw = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+        # dispatches of each kernel in the profiled run (one row per dispatch
+        # in the FETCH_SIZE pass): the general path's per-LED kernels run once
+        # per patch group, so bench.py turns per-dispatch bytes into bytes per
+        # LED step of the whole context with them
+        disp = {k: len(d["FETCH_SIZE"]) for k, d in acc.items() if "FETCH_SIZE" in d}
         stamp = src_hash()
     res = {"src_hash": stamp, "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
-           "derived": {}}
+           "derived": {}, "dispatches": disp}
     if perm and "k_meas_layout" in raw and "TCC_EA0_RDREQ_128B" in raw["k_meas_layout"]:
         # k_meas_layout_copy<256,16,64>: 4 blocks of 256 threads per Np 256 image (128 KiB read)
         known = sum(g // 1024 * 256 * 256 * 2.0 for g, _ in perm) / len(perm)
