@@ -458,13 +458,7 @@ int fpm_create(const fpm_problem *prob, int device, fpm_ctx **out) {
         } else {
             if ((rc = dalloc(c, &st.T, (size_t)B * nb * np))) return fail(rc);
         }
-        // the pupil numerator: fp16 beside the fp16 T of the Np 1024 register
-        // kernels (FPM_DP32=1 keeps it fp32), fp32 otherwise
-        if (reg1024 && fp16 && !getenv("FPM_DP32")) {
-            if ((rc = dalloc(c, &st.dP16, (size_t)B * nb * nb))) return fail(rc);
-        } else {
-            if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
-        }
+        if ((rc = dalloc(c, &st.dP, (size_t)B * nb * nb))) return fail(rc);
         if ((rc = dalloc(c, &st.rmax, (size_t)B * st.nty))) return fail(rc);
         // patch groups on concurrent streams (FPM_PATCH_GROUPS=n overrides):
         // two for the Np 1024 kernels, whose row launches cover a few patches

@@ -56,9 +56,6 @@ struct DevState {
     __half2 *T16;
     float *tsr, *tsc;
     float2 *dP;       // [B][nb][nb] pupil-update numerator (general path)
-    // Np 1024 with fp16 spectrum storage (config 5): the numerator held as
-    // __half2 [B][nb][nb] scaled by hscale like the spectrum (dP == nullptr then)
-    __half2 *dP16;
     float *tmax;      // [B][nty][ntx]
     unsigned *tdirty; // [B][ceil(ntx*nty/32)] fused path: tiles whose max is an upper bound
     float *rmax;      // [B][nty] general path: row maxima of tmax
@@ -103,7 +100,6 @@ inline DevState patch_view(const DevState &st, int b0, int n) {
     if (v.tsr) v.tsr += (size_t)b0 * st.nb;
     if (v.tsc) v.tsc += (size_t)b0 * st.np;
     if (v.dP) v.dP += b0 * nb2;
-    if (v.dP16) v.dP16 += b0 * nb2;
     if (v.tmax) v.tmax += (size_t)b0 * st.nty * st.ntx;
     if (v.tdirty) v.tdirty += (size_t)b0 * ((st.ntx * st.nty + 31) / 32);
     if (v.rmax) v.rmax += (size_t)b0 * st.nty;

@@ -222,30 +222,18 @@ __global__ void __launch_bounds__(kCommitThreads) k_pupil_commit(DevState st) {
     const int n = nb * nb, chunk = (n + st.npart - 1) / st.npart;
     const int i0 = part * chunk, i1 = min(n, i0 + chunk);
     float2 *pup = st.pupil + (size_t)b * nb * nb;
-    const float2 *dP = st.dP ? st.dP + (size_t)b * nb * nb : nullptr;
-    const __half2 *dP16 = st.dP16 ? st.dP16 + (size_t)b * nb * nb : nullptr;
+    const float2 *dP = st.dP + (size_t)b * nb * nb;
     // this thread's pixels (chunk <= kCommitPx) are loaded before the max
     // reduction, so their latency overlaps the rmax round trip
     constexpr int KP = kCommitPx / kCommitThreads;
     float2 pv[KP], dv[KP];
-    __half2 hd[KP];
     bool on[KP];
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
         const int i = i0 + threadIdx.x + k * kCommitThreads;
         on[k] = i < i1 && st.disk[i];
         pv[k] = on[k] ? pup[i] : make_float2(0.f, 0.f);
-        if (dP16)  // uniform (Np 1024 with fp16 storage): widened after the batch
-            hd[k] = dP16[on[k] ? i : 0];
-        else
-            dv[k] = on[k] ? dP[i] : make_float2(0.f, 0.f);
-    }
-    if (dP16) {
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {
-            const float2 h = __half22float2(hd[k]);
-            dv[k] = on[k] ? make_float2(h.x * st.hinv, h.y * st.hinv) : make_float2(0.f, 0.f);
-        }
+        dv[k] = on[k] ? dP[i] : make_float2(0.f, 0.f);
     }
     float m = 0.f;
     for (int i = threadIdx.x; i < st.nty; i += kCommitThreads) m = fmaxf(m, rmax[i]);

@@ -171,8 +171,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     const int rowc = row < nb ? row : nb - 1;  // rows past the box: in-bounds loads, discarded
     const int ky = rowc - r, w2 = r * r - ky * ky;
     float2 *pup = st.pupil + ((size_t)b * nb + rowc) * nb + r;        // indexed by kx
-    const float2 *dP = st.dP ? st.dP + ((size_t)b * nb + rowc) * nb + r : nullptr;
-    const __half2 *dP16 = st.dP16 ? st.dP16 + ((size_t)b * nb + rowc) * nb + r : nullptr;
+    const float2 *dP = st.dP + ((size_t)b * nb + rowc) * nb + r;
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;         // + kx (:358-362)
     float2 x[16];
     float pmx = 0.f;
@@ -186,7 +185,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
     // trips per row); all sixteen at once spilled 22 VGPRs.
     struct Half {
         float2 pv[8], dv[8], ov[8];
-        __half2 hv[8], hd[8];
+        __half2 hv[8];
         int kc[8];
     };
     auto load_half = [&](int hh, Half &q) {
@@ -195,12 +194,7 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
             const int kx = fold(4 * (t + 16 * (8 * hh + i)) + c);
             q.kc[i] = kx * kx <= w2 ? kx : 0;
             q.pv[i] = pup[q.kc[i]];
-            // unconditional (used only when commit): a branch here waited for
-            // the load; the fp16 numerator is widened after the batch (below)
-            if (dP16)  // uniform
-                q.hd[i] = dP16[q.kc[i]];
-            else
-                q.dv[i] = dP[q.kc[i]];
+            q.dv[i] = dP[q.kc[i]];  // unconditional (used only when commit): a branch here waited for the load
         }
         if (st.spec16) {  // uniform
             const __half2 *sp = st.spec16 + (size_t)b * st.L * st.L + srow;
@@ -243,13 +237,6 @@ __global__ void __launch_bounds__(n1k::NT) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
         if (hh == 1) load_half(1, q);  // behind the first half's pupil stores
-        if (dP16) {  // uniform: widen the fp16 numerator after all its loads
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float2 h = __half22float2(q.hd[i]);
-                q.dv[i] = make_float2(h.x * st.hinv, h.y * st.hinv);
-            }
-        }
         if (st.spec16) {  // uniform
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -468,8 +455,7 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
     }
     w1k_DN<false>(x, wt, twL, c, t, xrd);                                // :394 (rows)
     float2 *pup = st.pupil + ((size_t)b * nb + row) * nb + r;
-    float2 *dP = st.dP ? st.dP + ((size_t)b * nb + row) * nb + r : nullptr;
-    __half2 *dP16 = st.dP16 ? st.dP16 + ((size_t)b * nb + row) * nb + r : nullptr;
+    float2 *dP = st.dP + ((size_t)b * nb + row) * nb + r;
     const size_t srow = (size_t)(sa.yc + ky) * st.L + sa.xc;
     // the loads of half the row's pixels ahead of their stores (the stores may
     // alias the loads, so the compiler keeps program order: one memory latency
@@ -519,11 +505,7 @@ __global__ void __launch_bounds__(n1k::NT) k_rows1024_fwd(DevState st, StepArgs 
             const float2 dpc = cmul(cmul(D, cscale(cconj(pp), pa)), upd_coef_div(pa * pa + st.delta2, st.d2_im, pm));
             spec_st(st, b, si, cadd(o, dpc));
             const float oa = cmag(o);                            // pupil numerator (:459-464,469)
-            const float2 num = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
-            if (dP16)  // uniform: fp16 storage, the spectrum's scale
-                dP16[kx] = __float22half2_rn(make_float2(num.x * st.hscale, num.y * st.hscale));
-            else
-                dP[kx] = num;
+            dP[kx] = cmul(cmul(D, cscale(cconj(o), oa)), upd_coef_div(oa * oa + st.delta1, st.d1_im, 1.0f));
         }
     }
 }

@@ -285,11 +285,9 @@ def test_config5_fp16_storage_np1024_l4096():
         full = fpm_amd.Solver(fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=1))
         # the spectrum is the one L^2 buffer that shrinks (8 -> 4 bytes per
         # pixel); the Np 1024 row / column scratch T goes fp16 with it (8 -> 4
-        # bytes per element of [nb][Np]) plus its row and column scales, and
-        # the pupil numerator (8 -> 4 bytes per element of [nb][nb])
+        # bytes per element of [nb][Np]) plus its row and column scales
         nb = 2 * r + 1
-        assert full.info().device_bytes - s.info().device_bytes == \
-            4 * L * L + 4 * nb * Np - 4 * (nb + Np) + 4 * nb * nb
+        assert full.info().device_bytes - s.info().device_bytes == 4 * L * L + 4 * nb * Np - 4 * (nb + Np)
         full.close()
         s.upload(stack)
         s.init()

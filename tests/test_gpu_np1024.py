@@ -95,28 +95,6 @@ def test_np1024_fp16_scratch_vs_fp32_scratch():
             assert 0 < e < 2e-3, (k, b, e)
 
 
-def test_np1024_fp16_numerator_vs_fp32_numerator():
-    """fp16 spectrum storage keeps the Np 1024 pupil numerator in fp16 too
-    (scaled by the spectrum's power of two); FPM_DP32=1 keeps it fp32.  The
-    two differ by fp16 rounding of the numerator (2^-11 relative per element
-    of each LED's pupil increment), well inside config 5's 1e-2."""
-    L, r = 2048, 333
-    x0, y0, order = grid_geometry(Np, L, 2, 100)
-    stack = make_stack(Np, L, r, x0, y0, n_patch=2, seed=88)
-    prob = fpm_amd.Problem(Np, L, order, x0, y0, r, 5, 10, n_patch=2, flags=fpm_amd.FLAG_SPEC_FP16)
-    h = _run(prob, stack, 2)
-    os.environ["FPM_DP32"] = "1"
-    try:
-        f = _run(prob, stack, 2)
-    finally:
-        os.environ.pop("FPM_DP32", None)
-    for k in ("objF", "objCrop", "pupil"):
-        for b in range(2):
-            e = rel_l2(h[k][b], f[k][b])
-            print(f"np1024 fp16 vs fp32 numerator {k} patch {b} rel L2 {e:.2e}")
-            assert e < 2e-3, (k, b, e)
-
-
 @pytest.mark.parametrize("fp16", [False, True], ids=["fp32", "fp16"])
 def test_objcrop_l4096_six_step_equals_batched_transform(fp16):
     """objCrop at L 4096 (config 5): the six-step column IDFT (64 x 64, two
