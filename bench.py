@@ -163,9 +163,10 @@ def load_pmc(path, kernel, n_led=None):
                           "k_colpass_wave", "k_colpass_tiled", "k_rowfft_update_tiled", "k_tile_rows",
                           "k_pupil_commit") if k in pl]
         disp = d.get("dispatches", {})
-        if ks and n_led and all(k in disp for k in ks):
-            tot = sum(pl[k] * disp[k] for k in ks) / n_led
-            how = f"sum of per-dispatch bytes x dispatches / {n_led} LED steps of {', '.join(ks)}"
+        steps = n_led * d.get("bench_iterations", 1) if n_led else 0
+        if ks and steps and all(k in disp for k in ks):
+            tot = sum(pl[k] * disp[k] for k in ks) / steps
+            how = f"sum of per-dispatch bytes x dispatches / {steps} LED steps of {', '.join(ks)}"
         else:
             tot = sum(pl[k] for k in ks) if ks else None
             how = f"sum of per-dispatch bytes of {', '.join(ks)} (one patch group's LED step)"

@@ -18,5 +18,7 @@ for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDRE
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex "$RX" --output-format csv -d $OUT/p$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-gather ${BENCH_ARGS:-} > $OUT/p$i.log 2>&1 || { echo "pass $i rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/pmc_to_json.py $OUT $OUT/pmc.json > $OUT/pmc_summary.txt
+# the profiled run is one iteration (--steps 1 --warmup 0): recorded in the
+# file, bench.py divides a kernel's dispatches by it
+PMC_BENCH_ITERS=1 python3 tools/pmc_to_json.py $OUT $OUT/pmc.json > $OUT/pmc_summary.txt
 rm -rf $OUT/p[0-9]*/   # raw rocprofv3 output: too large to copy back; pmc.json keeps the per-kernel means

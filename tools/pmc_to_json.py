@@ -100,7 +100,9 @@ def main():
             prev = json.load(fh)
         raw, stamp = prev["raw_per_launch"], prev["src_hash"]
         disp = prev.get("dispatches", {})
+        iters = prev.get("bench_iterations", 1)
     else:
+        iters = 1
         for f in sorted(glob.glob(os.path.join(src, "*", "**", "*counter_collection.csv"), recursive=True)):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
@@ -117,7 +119,9 @@ def main():
         disp = {k: len(d["FETCH_SIZE"]) for k, d in acc.items() if "FETCH_SIZE" in d}
         stamp = src_hash()
     res = {"src_hash": stamp, "raw_per_launch": raw, "per_launch_hbm_bytes": {}, "read_scale": {},
-           "derived": {}, "dispatches": disp}
+           "derived": {}, "dispatches": disp,
+           # iterations of the profiled bench run (tools/gpu/prof_counters.sh: 1)
+           "bench_iterations": int(os.environ.get("PMC_BENCH_ITERS", iters))}
     if perm and "k_meas_layout" in raw and "TCC_EA0_RDREQ_128B" in raw["k_meas_layout"]:
         # k_meas_layout_copy<256,16,64>: 4 blocks of 256 threads per Np 256 image (128 KiB read)
         known = sum(g // 1024 * 256 * 256 * 2.0 for g, _ in perm) / len(perm)
